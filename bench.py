@@ -1,0 +1,220 @@
+"""Headline benchmark: utterances/sec of embedding extraction (80-d FBANK, T=200)
+on res2net50_w24_s4_c32 (BASELINE.json configs[2]; the north_star's MFMA
+target), one process per GPU, inputs resident in HBM.
+
+A "step" = one forward of one batch of B synthetic utterances through the
+whole hot path (input cast -> stem -> 16 Res2Net bottlenecks -> stats-pool ->
+BN/dense/BN head); with N > 1 ranks each step also all-gathers the step's
+embeddings over RCCL (the cohort assembly of eval_inference_model.sh:38-39).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+       torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+
+from __future__ import annotations
+
+import argparse
+import io
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_F32_TFLOPS = 157.3     # f32-input MFMA = vector rate
+PEAK_HBM_GBS = 8000.0       # HBM3E spec
+
+
+def _kernel_name(tag, dt):
+    kind = tag & 15
+    if tag & (1 << 14):
+        wco, wpx, vec = (tag >> 4) & 15, (tag >> 8) & 15, (tag >> 12) & 1
+        t = "float" if tag & (1 << 13) else "__bf16"
+        return f"conv_igemm<{t}, {wco}, {wpx}, {'true' if vec else 'false'}>"
+    return {1: "stats_pool_k", 2: "splitk_reduce", 3: "other"}.get(kind, "other")
+
+
+def weights_blob(model, feat_dim, cache_dir):
+    from voxsrc2020_speaker_verification_amd import archs, synth, weights
+    path = os.path.join(cache_dir, f"voxemb_{model}_{feat_dim}_seed1.blob")
+    if os.path.exists(path):
+        with open(path, "rb") as f:
+            return f.read()
+    spec = archs.get_arch(model, feat_dim)
+    t = synth.make_weights(spec, seed=1)
+    buf = io.BytesIO()
+    weights.save_blob(buf, spec, t)
+    data = buf.getvalue()
+    try:
+        os.makedirs(cache_dir, exist_ok=True)
+        tmp = path + f".{os.getpid()}"
+        with open(tmp, "wb") as f:
+            f.write(data)
+        os.replace(tmp, path)
+    except OSError:
+        pass
+    return data
+
+
+def cpu_baseline(model, feat_dim, T, blob, budget_s=12.0):
+    """The numpy fp32 oracle (kind "port") on a bounded sample."""
+    from oracle import models_ref
+    from voxsrc2020_speaker_verification_amd import synth, weights
+    spec, t = weights.load_blob(blob)
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max([i.get("num_threads", 1) for i in threadpool_info()
+                     if i.get("user_api") == "blas"] or [1])
+    except Exception:
+        cores = os.cpu_count() or 1
+    bs = 4
+    x = synth.make_features(bs, T, feat_dim, seed=99)
+    n, t0 = 0, time.perf_counter()
+    while True:
+        models_ref.forward(spec, t, x)
+        n += bs
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    el = time.perf_counter() - t0
+    return {"value": n / el, "unit": "utterances/sec", "cores": int(cores), "kind": "port",
+            "sample": f"{n} utterances of {T}x{feat_dim} in batches of {bs} "
+                      f"({el:.1f} s, numpy fp32 oracle, BLAS threads={cores})"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--model", default="res2net50_w24_s4_c32")
+    ap.add_argument("--feat-dim", type=int, default=80)
+    ap.add_argument("--frames", type=int, default=200)
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cache-dir", default=os.environ.get("VOXEMB_CACHE", "/tmp/voxemb_cache"))
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", local if world > 1 else 0)
+
+    from voxsrc2020_speaker_verification_amd import synth
+    from voxsrc2020_speaker_verification_amd.extractor import Extractor
+
+    blob = weights_blob(args.model, args.feat_dim, args.cache_dir)
+    ex = Extractor(blob, device=dev.index, precision=args.precision)
+    B, T, F = args.batch, args.frames, args.feat_dim
+    x = torch.from_numpy(synth.make_features(B, T, F, seed=1000 + rank)).to(dev)
+    out = torch.empty((B, ex.dim), dtype=torch.float32, device=dev)
+    gathered = [torch.empty_like(out) for _ in range(world)] if world > 1 else None
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        ex.run_device(x, out, stream)
+        if world > 1:
+            dist.all_gather(gathered, out)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    ms_per_step = el * 1000.0 / args.steps
+    value = world * B * args.steps / el
+
+    # ---- per-kernel timing (HIP events around every launch, same stream)
+    prof = ex.profile(x, reps=5, stream=stream)
+    groups = {}
+    for ms, fl, by, tag in zip(prof["ms"], prof["flops"], prof["bytes"], prof["kind"]):
+        g = groups.setdefault(_kernel_name(int(tag), args.precision),
+                              {"ms": 0.0, "flops": 0.0, "bytes": 0.0, "n": 0, "kind": int(tag) & 15})
+        g["ms"] += float(ms)
+        g["flops"] += float(fl)
+        g["bytes"] += float(by)
+        g["n"] += 1
+    conv = {k: v for k, v in groups.items() if k.startswith("conv_igemm")}
+    dom_name, dom = max(conv.items(), key=lambda kv: kv[1]["ms"])
+    peak = PEAK_F32_TFLOPS if "float" in dom_name else PEAK_BF16_TFLOPS
+    ach = (dom["flops"] / dom["n"]) / (dom["ms"] / dom["n"] * 1e-3) / 1e12
+    fwd_ms = float(np.sum(prof["ms"]))
+    conv_fl = sum(v["flops"] for v in conv.values())
+    conv_ms = sum(v["ms"] for v in conv.values())
+    pool = groups.get("stats_pool_k")
+    roof = {"bound": "mfma", "kernel": dom_name, "launches_per_step": dom["n"],
+            "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
+            "frac": round(ach / peak, 4), "traffic": None,
+            "avg_launch_us": round(dom["ms"] / dom["n"] * 1e3, 2),
+            "flop_per_launch": dom["flops"] / dom["n"]}
+    extra = {
+        "conv_stack": {"achieved_tflops": round(conv_fl / (conv_ms * 1e-3) / 1e12, 2),
+                       "frac": round(conv_fl / (conv_ms * 1e-3) / 1e12 / peak, 4),
+                       "ms": round(conv_ms, 3), "flop": conv_fl},
+        "forward_ms_profiled": round(fwd_ms, 3),
+        "kernels": {k: {"n": v["n"], "ms": round(v["ms"], 4),
+                        "tflops": round(v["flops"] / max(v["ms"], 1e-9) / 1e9, 2) if v["flops"] else None,
+                        "gbs": round(v["bytes"] / max(v["ms"], 1e-9) / 1e6, 1)}
+                    for k, v in sorted(groups.items(), key=lambda kv: -kv[1]["ms"])},
+    }
+    if pool:
+        gbs = pool["bytes"] / pool["n"] / (pool["ms"] / pool["n"] * 1e-3) / 1e9
+        extra["stats_pool_roofline"] = {"bound": "hbm", "achieved": round(gbs, 1),
+                                        "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                                        "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": None,
+                                        "bytes_per_launch": pool["bytes"] / pool["n"]}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.model, F, T, blob)
+
+    if rank == 0:
+        line = {
+            "metric": "utterances/sec (80-d FBANK, T=200) embedding extraction",
+            "value": round(value, 1), "unit": "utterances/sec", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": args.precision, "data": "synthetic (seeded N(0,1) FBANK, random-init "
+                                            "calibrated weights)",
+            "config": {"workload": f"{args.model} {F}x{T} extraction", "global_batch": B * world,
+                       "per_gpu_batch": B, "frames": T, "feat_dim": F,
+                       "parallelism": f"dp{world}" + (" + RCCL all-gather" if world > 1 else "")},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            **extra,
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    ex.close()
+
+
+if __name__ == "__main__":
+    main()

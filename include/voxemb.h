@@ -1,0 +1,114 @@
+/*
+ * voxemb.h -- C-ABI of libvoxemb.so, the MI355X (gfx950) speaker-embedding
+ * extractor that replaces the TF1 frozen-graph forward of
+ * xx205/voxsrc2020_speaker_verification's `tensorflow/tf_extract.py`.
+ *
+ * Plain pointers and sizes only; no torch / HIP types cross the boundary
+ * (streams are passed as `void*` = hipStream_t, NULL = the handle's stream).
+ * Every function returns VOX_OK (0) or a negative status; the thread-local
+ * message is available from vox_last_error().  Ownership: callers own every
+ * buffer they pass in; the handle owns its device weights and workspace.
+ *
+ * Reference interfaces replaced (file:line under the reference repo):
+ *   vox_load / vox_load_blob  <- tf.GraphDef().ParseFromString + import_graph_def
+ *                                (tensorflow/tf_extract.py:75-82)
+ *   vox_dim                   <- width of tensor "model/outputs:0"
+ *                                (tensorflow/models/res2net_model.py:242,
+ *                                 tdnn_model.py:153, dpn_model.py:168)
+ *   vox_embed                 <- sess.run(model/outputs:0, {model/inputs:0: x})
+ *                                (tensorflow/tf_extract.py:108); x is the
+ *                                [N,T,F] batch before tf_extract's expand_dims
+ *                                (tf_extract.py:32)
+ *   vox_embed_device          <- same, inputs already resident in HBM
+ *   vox_embed_utt             <- the chunk loop + length-weighted average
+ *                                (tensorflow/tf_extract.py:96-111)
+ *   vox_stats_pool_device     <- stats_pool (tensorflow/models/models.py:262-269)
+ *                                followed by the head's first BN
+ *                                (res2net_model.py:239)
+ *   vox_sliding_cmn           <- Kaldi `apply-cmvn-sliding --norm-vars=false
+ *                                --center=true --cmn-window=300`
+ *                                (tensorflow/tf_extract.py:63)
+ *   vox_mat_shape/vox_read_mat<- kaldi_io.read_mat / _read_mat_binary /
+ *                                _read_compressed_mat (tensorflow/kaldi_io.py:420-504)
+ *   vox_format_vec_flt        <- kaldi_io.write_vec_flt (kaldi_io.py:304-334)
+ *                                + `copy-vector ark:- ark,scp:` (tf_extract.py:65)
+ */
+#ifndef VOXEMB_H
+#define VOXEMB_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VOX_OK 0
+#define VOX_EINVAL (-22)   /* bad argument / shape mismatch                 */
+#define VOX_ENOMEM (-12)   /* host or device allocation failed              */
+#define VOX_EIO (-5)       /* file missing / malformed blob / bad ark       */
+#define VOX_ESHORT (-61)   /* utterance shorter than 25 frames: the reference
+                              raises ZeroDivisionError (tf_extract.py:102,111) */
+#define VOX_EHIP (-1000)   /* HIP runtime error                             */
+
+#define VOX_FP32 0         /* fp32 activations, f32-input MFMA (parity mode) */
+#define VOX_BF16 1         /* bf16 activations, bf16 MFMA, fp32 accumulate   */
+
+typedef struct vox_model vox_model;
+
+/* Load a VOXEMB01 weight blob (file or memory) onto HIP device `device`. */
+int vox_load(const char* blob_path, int device, int precision, vox_model** out);
+int vox_load_blob(const void* blob, size_t nbytes, int device, int precision,
+                  vox_model** out);
+void vox_free(vox_model* m);
+
+int vox_dim(const vox_model* m);         /* embedding width (256 / 192)      */
+int vox_feat_dim(const vox_model* m);    /* expected F (mel bins)            */
+int vox_expand_dim(const vox_model* m);  /* 2 = TDNN layout, 3 = 2-D layout  */
+int vox_precision(const vox_model* m);
+
+/* x: host [n,t,f] float32 row-major; out: host [n, vox_dim] float32. */
+int vox_embed(vox_model* m, const float* x, int n, int t, int f, float* out);
+/* d_x, d_out: device pointers on the handle's device; stream may be NULL. */
+int vox_embed_device(vox_model* m, const float* d_x, int n, int t, int f,
+                     float* d_out, void* stream);
+/* One utterance of any length t >= 25, chunked at 1000 frames. */
+int vox_embed_utt(vox_model* m, const float* x, int t, int f, float* out);
+
+/* Per-op profile of one forward at (n, t): runs the plan `reps` times with
+ * HIP events around every op on `stream`.  Fills up to `max_ops` entries:
+ * op_ms (average ms per launch), op_flops (algorithmic FLOP per launch),
+ * op_bytes (algorithmic HBM bytes per launch), op_kind (0 conv, 1 stats-pool,
+ * 2 head, 3 other).  Returns the number of ops (>=0) or a status (<0). */
+int vox_profile(vox_model* m, const float* d_x, int n, int t, int f, int reps,
+                float* op_ms, double* op_flops, double* op_bytes, int* op_kind,
+                int max_ops, void* stream);
+
+/* Standalone stats-pool (+BN) kernel: x NHWC [n,h,w,c] (dtype VOX_FP32 or
+ * VOX_BF16), mean/inv per pooled feature (may be NULL = identity),
+ * out [n, w*2c] float32 with feature index w*2c + {c | c+C}. */
+int vox_stats_pool_device(const void* d_x, int dtype, int n, int h, int w, int c,
+                          const float* d_mean, const float* d_inv, float* d_out,
+                          void* stream);
+
+const char* vox_last_error(void);
+
+/* ---- host-side Kaldi I/O (no Kaldi binaries needed) --------------------- */
+int vox_sliding_cmn(const float* in, int t, int f, int cmn_window, int center,
+                    float* out);
+/* Binary Kaldi matrix ("\0B" + FM/DM/CM) at byte `offset` of `path`. */
+int vox_mat_shape(const char* path, int64_t offset, int* rows, int* cols);
+int vox_read_mat(const char* path, int64_t offset, float* out, int rows, int cols);
+/* Same, from memory: `buf` starts at "\0B". */
+int vox_parse_mat(const uint8_t* buf, size_t nbytes, float* out, int rows, int cols,
+                  size_t* consumed);
+int vox_parse_mat_shape(const uint8_t* buf, size_t nbytes, int* rows, int* cols);
+/* Serialise "key \0BFV \4<u32 dim><dim f32>" into buf; returns bytes written
+ * (or needed, if cap is too small) and the offset of "\0B" via *data_offset. */
+int64_t vox_format_vec_flt(const char* key, const float* v, int dim, uint8_t* buf,
+                           size_t cap, int64_t* data_offset);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VOXEMB_H */

@@ -1,0 +1,915 @@
+// libvoxemb host runtime: weight blob -> device weights, per-shape execution
+// plans (one kernel launch per op, pointers into grow-only device slots),
+// C-ABI entry points declared in include/voxemb.h.
+//
+// Graph semantics follow the reference TF1 builders:
+//   TDNN    tensorflow/models/tdnn_model.py:24-30,128-161
+//   Res2Net tensorflow/models/res2net_model.py:26-136,185-243
+//   DPN     tensorflow/models/dpn_model.py:24-171
+//   head    res2net_model.py:229-242 / models.py:262-269,306-309
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <memory>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "../../include/voxemb.h"
+#include "kernels.h"
+
+using namespace vox;
+
+static thread_local std::string g_err;
+static int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+#define HIPCHK(expr)                                                                 \
+  do {                                                                               \
+    hipError_t e_ = (expr);                                                          \
+    if (e_ != hipSuccess)                                                            \
+      return fail(VOX_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_));      \
+  } while (0)
+
+extern "C" const char* vox_last_error(void) { return g_err.c_str(); }
+int vox_set_error(int code, const char* msg) { return fail(code, msg); }
+
+static const float kEps4 = 1.001e-5f;  // fused BN eps clamp (models.py:62-67)
+static const float kEps2 = 1e-5f;      // non-fused 2-D head BN (models.py:20)
+
+// ------------------------------------------------------------------ blob
+struct HostTensor {
+  std::string name, kind;
+  std::vector<int> shape;
+  std::vector<float> data;
+};
+
+struct Spec {
+  std::map<std::string, std::string> kv;
+  std::string get(const std::string& k) const {
+    auto it = kv.find(k);
+    return it == kv.end() ? std::string() : it->second;
+  }
+  int geti(const std::string& k, int dflt = -1) const {
+    auto s = get(k);
+    return s.empty() ? dflt : std::atoi(s.c_str());
+  }
+  std::vector<int> getv(const std::string& k) const {
+    std::vector<int> v;
+    std::stringstream ss(get(k));
+    std::string item;
+    while (std::getline(ss, item, ','))
+      if (!item.empty()) v.push_back(std::atoi(item.c_str()));
+    return v;
+  }
+};
+
+static int parse_blob(const uint8_t* raw, size_t n, Spec& spec, std::vector<HostTensor>& ts) {
+  if (n < 16 || std::memcmp(raw, "VOXEMB01", 8) != 0) return fail(VOX_EIO, "not a VOXEMB01 blob");
+  uint64_t hlen;
+  std::memcpy(&hlen, raw + 8, 8);
+  if (16 + hlen > n) return fail(VOX_EIO, "truncated blob header");
+  std::string header((const char*)raw + 16, hlen);
+  size_t data_start = (16 + hlen + 63) / 64 * 64;
+  std::stringstream ss(header);
+  std::string line;
+  int ntensors = -1;
+  while (std::getline(ss, line)) {
+    if (line.empty()) continue;
+    if (ntensors < 0) {
+      auto eq = line.find('=');
+      if (eq == std::string::npos) return fail(VOX_EIO, "bad header line: " + line);
+      std::string k = line.substr(0, eq), v = line.substr(eq + 1);
+      if (k == "tensors") {
+        ntensors = std::atoi(v.c_str());
+      } else {
+        spec.kv[k] = v;
+      }
+      continue;
+    }
+    // name|kind|dims|offset|nbytes
+    std::vector<std::string> f;
+    std::stringstream ls(line);
+    std::string item;
+    while (std::getline(ls, item, '|')) f.push_back(item);
+    if (f.size() != 5) return fail(VOX_EIO, "bad tensor line: " + line);
+    HostTensor t;
+    t.name = f[0];
+    t.kind = f[1];
+    std::stringstream ds(f[2]);
+    size_t numel = 1;
+    while (std::getline(ds, item, ',')) {
+      t.shape.push_back(std::atoi(item.c_str()));
+      numel *= t.shape.back();
+    }
+    size_t off = std::strtoull(f[3].c_str(), nullptr, 10);
+    size_t nb = std::strtoull(f[4].c_str(), nullptr, 10);
+    if (nb != numel * 4 || data_start + off + nb > n)
+      return fail(VOX_EIO, "tensor out of range: " + t.name);
+    t.data.resize(numel);
+    std::memcpy(t.data.data(), raw + data_start + off, nb);
+    ts.push_back(std::move(t));
+  }
+  if (ntensors < 0 || (int)ts.size() != ntensors) return fail(VOX_EIO, "tensor count mismatch");
+  return VOX_OK;
+}
+
+// ------------------------------------------------------------------ device memory
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+  hipError_t ensure(size_t b) {
+    if (b <= bytes) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+    hipError_t e = hipMalloc(&p, b);
+    if (e == hipSuccess) bytes = b;
+    return e;
+  }
+};
+
+static uint16_t f2bf(float f) {  // round-to-nearest-even (weights only; no NaN here)
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  u += 0x7FFF + ((u >> 16) & 1);
+  return (uint16_t)(u >> 16);
+}
+
+// A convolution with its BN, in kernel-native layout.
+struct ConvW {
+  int kh = 1, kw = 1, cin = 0, cout = 0, groups = 1;  // cin/cout per group
+  int coutp = 0, cinp = 0, kp = 0, wco = 1, vec = 1;
+  std::shared_ptr<DevBuf> w;         // [groups][coutp][kp] in the model dtype
+  std::shared_ptr<DevBuf> mean, inv; // optional epilogue BN (cout*groups)
+};
+
+struct BNW {
+  int c = 0;
+  std::shared_ptr<DevBuf> mean, inv;
+};
+
+static int choose_wco(int cout_tiles) {
+  if (cout_tiles <= 4) return cout_tiles;
+  if (cout_tiles <= 6) return 6;
+  if (cout_tiles <= 8) return 8;
+  if (cout_tiles % 6 == 0 && cout_tiles % 8 != 0) return 6;
+  return 8;
+}
+
+// ------------------------------------------------------------------ plan
+enum OpKind { OP_CONV = 0, OP_POOL = 1, OP_HEAD = 2, OP_OTHER = 3 };
+struct Op {
+  int kind = OP_CONV;
+  int type = 0;  // 0 conv, 1 splitk reduce, 2 stats pool, 3 avgpool, 4 convert
+  ConvParams cp{};
+  ConvLaunch cl{};
+  // reduce
+  const float* part = nullptr; int S = 0, M = 0, coutp = 0, cout = 0, flags = 0;
+  const float* mean = nullptr; const float* inv = nullptr; float* out = nullptr; int ldo = 0;
+  // pool / avgpool / convert
+  const void* src = nullptr; void* dst = nullptr; int N = 0, H = 0, W = 0, C = 0, lds = 0, ldd = 0,
+             Ho = 0, Wo = 0;
+  int64_t count = 0;
+  double flops = 0, bytes = 0;
+};
+
+enum Slot { S_IN, S_X0, S_X1, S_A, S_B, S_SC, S_POOL, S_PART, S_NSLOTS };
+
+struct vox_model {
+  int device = 0;
+  DType dt = BF16;
+  Spec spec;
+  std::string family;
+  int feat_dim = 0, out_dim = 0, expand_dim = 3, pooled = 0;
+  std::vector<ConvW> convs;  // consumption order
+  std::vector<BNW> bns;      // standalone BNs (prologues, pool BN, DPN final)
+  ConvW head;                // dense as a 1x1 conv, fp32
+  BNW head_bn1;
+  DevBuf slots[S_NSLOTS];
+  size_t slot_need[S_NSLOTS] = {};
+  hipStream_t stream = nullptr;
+  // plan cache
+  int plan_n = -1, plan_t = -1;
+  const float* plan_x = nullptr;
+  float* plan_out = nullptr;
+  std::vector<Op> plan;
+  DevBuf stage_in, stage_out;  // host-API staging
+};
+
+static size_t esize(DType t) { return t == BF16 ? 2 : 4; }
+
+// Upload one HWIO conv kernel (+ optional BN) in kernel-native layout.
+static int make_conv(vox_model* m, const HostTensor& k, int groups, const HostTensor* bm,
+                     const HostTensor* bv, float eps, DType dt, ConvW& out, int col0 = 0,
+                     int ncols = -1) {
+  const int kh = k.shape[0], kw = k.shape[1], cin = k.shape[2];
+  const int cout_all = k.shape[3];
+  if (ncols < 0) ncols = cout_all;
+  const int cout = ncols / groups;
+  const int taps = kh * kw;
+  const int KS = conv_kstep(dt), VN = conv_vec(dt);
+  out.kh = kh; out.kw = kw; out.cin = cin; out.cout = cout; out.groups = groups;
+  out.vec = (cin % VN == 0) ? 1 : 0;
+  const int tiles = (cout + 15) / 16;
+  out.wco = choose_wco(tiles);
+  out.coutp = ((cout + 16 * out.wco - 1) / (16 * out.wco)) * 16 * out.wco;
+  if (out.vec) {
+    out.cinp = (cin + KS - 1) / KS * KS;
+    out.kp = taps * out.cinp;
+  } else {
+    out.cinp = cin;
+    out.kp = (taps * cin + KS - 1) / KS * KS;
+  }
+  const size_t per_g = (size_t)out.coutp * out.kp;
+  std::vector<float> w(per_g * groups, 0.f);
+  for (int g = 0; g < groups; ++g)
+    for (int co = 0; co < cout; ++co)
+      for (int t = 0; t < taps; ++t)
+        for (int ci = 0; ci < cin; ++ci) {
+          const int ky = t / kw, kx = t % kw;
+          const float v = k.data[(((size_t)ky * kw + kx) * cin + ci) * cout_all + col0 + g * cout + co];
+          const size_t kidx = out.vec ? (size_t)t * out.cinp + ci : (size_t)t * cin + ci;
+          w[g * per_g + (size_t)co * out.kp + kidx] = v;
+        }
+  out.w = std::make_shared<DevBuf>();
+  const size_t es = esize(dt);
+  HIPCHK(out.w->ensure(w.size() * es));
+  if (dt == BF16) {
+    std::vector<uint16_t> h(w.size());
+    for (size_t i = 0; i < w.size(); ++i) h[i] = f2bf(w[i]);
+    HIPCHK(hipMemcpy(out.w->p, h.data(), h.size() * 2, hipMemcpyHostToDevice));
+  } else {
+    HIPCHK(hipMemcpy(out.w->p, w.data(), w.size() * 4, hipMemcpyHostToDevice));
+  }
+  if (bm) {
+    const int C = (int)bm->data.size();
+    std::vector<float> inv(C);
+    for (int c = 0; c < C; ++c) inv[c] = 1.0f / std::sqrt(bv->data[c] + eps);
+    out.mean = std::make_shared<DevBuf>();
+    out.inv = std::make_shared<DevBuf>();
+    HIPCHK(out.mean->ensure(C * 4));
+    HIPCHK(out.inv->ensure(C * 4));
+    HIPCHK(hipMemcpy(out.mean->p, bm->data.data(), C * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(out.inv->p, inv.data(), C * 4, hipMemcpyHostToDevice));
+  }
+  return VOX_OK;
+}
+
+static int make_bn(const HostTensor& bm, const HostTensor& bv, float eps, BNW& out, int off = 0,
+                   int len = -1) {
+  if (len < 0) len = (int)bm.data.size();
+  std::vector<float> inv(len);
+  for (int c = 0; c < len; ++c) inv[c] = 1.0f / std::sqrt(bv.data[off + c] + eps);
+  out.c = len;
+  out.mean = std::make_shared<DevBuf>();
+  out.inv = std::make_shared<DevBuf>();
+  HIPCHK(out.mean->ensure(len * 4));
+  HIPCHK(out.inv->ensure(len * 4));
+  HIPCHK(hipMemcpy(out.mean->p, bm.data.data() + off, len * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(out.inv->p, inv.data(), len * 4, hipMemcpyHostToDevice));
+  return VOX_OK;
+}
+
+struct Cursor {
+  const std::vector<HostTensor>& ts;
+  size_t i = 0;
+  explicit Cursor(const std::vector<HostTensor>& t) : ts(t) {}
+  const HostTensor* next(const char* kind_hint) {
+    if (i >= ts.size()) {
+      g_err = std::string("blob exhausted, expected ") + kind_hint;
+      return nullptr;
+    }
+    return &ts[i++];
+  }
+};
+
+#define NEXT(var, hint)                                  \
+  const HostTensor* var = cur.next(hint);                \
+  if (!var) return VOX_EIO;
+
+static int load_weights(vox_model* m, const std::vector<HostTensor>& ts) {
+  Cursor cur(ts);
+  const DType dt = m->dt;
+  int rc;
+  auto conv_bn = [&](float eps, ConvW& cw) -> int {
+    const HostTensor* k = cur.next("conv");
+    const HostTensor* bm = cur.next("bn mean");
+    const HostTensor* bv = cur.next("bn var");
+    if (!k || !bm || !bv) return VOX_EIO;
+    return make_conv(m, *k, 1, bm, bv, eps, dt, cw);
+  };
+  if (m->family == "tdnn") {
+    for (size_t l = 0; l < m->spec.getv("filters").size(); ++l) {
+      ConvW cw;
+      if ((rc = conv_bn(kEps4, cw))) return rc;
+      m->convs.push_back(cw);
+    }
+  } else if (m->family == "res2net") {
+    const int s = m->spec.geti("split");
+    auto blocks = m->spec.getv("block_sizes");
+    ConvW stem;
+    if ((rc = conv_bn(kEps4, stem))) return rc;
+    m->convs.push_back(stem);
+    for (size_t st = 0; st < blocks.size(); ++st)
+      for (int b = 0; b < blocks[st]; ++b) {
+        if (b == 0) {
+          ConvW pr;
+          if ((rc = conv_bn(kEps4, pr))) return rc;
+          m->convs.push_back(pr);
+        }
+        ConvW a;
+        if ((rc = conv_bn(kEps4, a))) return rc;
+        m->convs.push_back(a);
+        NEXT(k, "split kernel");
+        const int w = k->shape[2];
+        for (int j = 0; j < s - 1; ++j) {
+          NEXT(bm, "split bn mean");
+          NEXT(bv, "split bn var");
+          ConvW br;
+          if ((rc = make_conv(m, *k, 1, bm, bv, kEps4, dt, br, j * w, w))) return rc;
+          m->convs.push_back(br);
+        }
+        ConvW c;
+        if ((rc = conv_bn(kEps4, c))) return rc;
+        m->convs.push_back(c);
+      }
+  } else if (m->family == "dpn") {
+    const int G = m->spec.geti("cardinality");
+    ConvW stem;
+    if ((rc = conv_bn(kEps4, stem))) return rc;
+    m->convs.push_back(stem);
+    // every body conv is BN->ReLU->conv: BN becomes the conv's prologue
+    auto ks = m->spec.getv("k_sec");
+    for (size_t st = 0; st < ks.size(); ++st)
+      for (int b = 0; b < ks[st]; ++b) {
+        const int nconv = (b == 0) ? 4 : 3;
+        for (int j = 0; j < nconv; ++j) {
+          NEXT(bm, "bn mean");
+          NEXT(bv, "bn var");
+          NEXT(k, "conv");
+          BNW pro;
+          if ((rc = make_bn(*bm, *bv, kEps4, pro))) return rc;
+          m->bns.push_back(pro);
+          ConvW cw;
+          const int groups = (k->shape[0] == 3) ? G : 1;
+          if ((rc = make_conv(m, *k, groups, nullptr, nullptr, kEps4, dt, cw))) return rc;
+          m->convs.push_back(cw);
+        }
+      }
+    NEXT(fm, "final bn mean");
+    NEXT(fv, "final bn var");
+    BNW fin;
+    if ((rc = make_bn(*fm, *fv, kEps4, fin))) return rc;
+    m->bns.push_back(fin);
+  } else {
+    return fail(VOX_EINVAL, "unknown family " + m->family);
+  }
+  // head: BN(2-D) -> dense -> BN(2-D), dense in fp32 as a 1x1 conv
+  NEXT(h1m, "head bn1 mean");
+  NEXT(h1v, "head bn1 var");
+  NEXT(dk, "dense kernel");
+  NEXT(h2m, "head bn2 mean");
+  NEXT(h2v, "head bn2 var");
+  if ((rc = make_bn(*h1m, *h1v, kEps2, m->head_bn1))) return rc;
+  HostTensor dk4 = *dk;  // [D, out] -> HWIO [1,1,D,out]
+  dk4.shape = {1, 1, dk->shape[0], dk->shape[1]};
+  if ((rc = make_conv(m, dk4, 1, h2m, h2v, kEps2, F32, m->head))) return rc;
+  m->pooled = dk->shape[0];
+  m->out_dim = dk->shape[1];
+  if (cur.i != ts.size()) return fail(VOX_EIO, "blob has trailing tensors");
+  return VOX_OK;
+}
+
+// ------------------------------------------------------------------ plan builder
+struct Builder {
+  vox_model* m;
+  bool dry;
+  std::vector<Op>* ops;
+  char* base(Slot s, size_t bytes) {
+    m->slot_need[s] = std::max(m->slot_need[s], bytes);
+    return dry ? nullptr : (char*)m->slots[s].p;
+  }
+};
+
+struct Act {  // an NHWC activation view
+  const void* p;
+  int ld, N, H, W, C;
+};
+
+static size_t es_of(vox_model* m) { return esize(m->dt); }
+
+static void emit_conv(Builder& B, const ConvW& cw, Act x, const void* x2, int ldx2, int sh,
+                      int sw, int dh, int dw, int ph, int pw, int Ho, int Wo, void* y, int ldy,
+                      int flags, const void* res = nullptr, int ldr = 0, void* y2 = nullptr,
+                      int ldy2 = 0, int ysplit = 1 << 30, const float* in_mean = nullptr,
+                      const float* in_inv = nullptr, DType dt_override = (DType)-1) {
+  Op op;
+  op.kind = OP_CONV;
+  op.type = 0;
+  ConvParams& p = op.cp;
+  p.x = x.p; p.ldx = x.ld; p.x2 = x2; p.ldx2 = ldx2;
+  p.in_mean = in_mean; p.in_inv = in_inv;
+  p.w = cw.w->p; p.kp = cw.kp;
+  p.y = y; p.ldy = ldy; p.y2 = y2; p.ldy2 = ldy2; p.ysplit = ysplit;
+  p.res = res; p.ldr = ldr;
+  p.mean = cw.mean ? (const float*)cw.mean->p : nullptr;
+  p.inv = cw.inv ? (const float*)cw.inv->p : nullptr;
+  p.partial = nullptr;
+  p.N = x.N; p.H = x.H; p.W = x.W; p.Cin = cw.cin; p.Ho = Ho; p.Wo = Wo; p.Cout = cw.cout;
+  p.coutp = cw.coutp;
+  p.kh = cw.kh; p.kw = cw.kw; p.sh = sh; p.sw = sw; p.dh = dh; p.dw = dw; p.ph = ph; p.pw = pw;
+  p.cinp = cw.cinp; p.kchunk = 0; p.flags = flags;
+  p.groups = cw.groups;
+  p.cblocks = cw.coutp / (16 * cw.wco);
+  p.fast4 = (cw.cout % 4 == 0 && ldy % 4 == 0 && (ysplit >= (1 << 30) || (ysplit % 4 == 0 && ldy2 % 4 == 0)) &&
+             (!res || ldr % 4 == 0) && cw.groups == 1) ? 1 : 0;
+  op.cl.wco = cw.wco;
+  op.cl.vec = cw.vec;
+  op.cl.splitk = 1;
+  const int M = x.N * Ho * Wo;
+  op.cl.wpx = M >= 64 * 4 * 512 ? 4 : (M >= 64 * 2 * 256 ? 2 : 1);
+  const double es = dt_override == F32 ? 4.0 : (double)es_of(B.m);
+  op.flops = 2.0 * M * cw.cout * cw.groups * (double)cw.kh * cw.kw * cw.cin;
+  op.bytes = es * ((double)x.N * x.H * x.W * cw.cin * cw.groups * (x2 ? 2 : 1) +
+                   (double)M * cw.cout * cw.groups * (res ? 2 : 1));
+  B.ops->push_back(op);
+}
+
+static void emit_pool(Builder& B, Act x, float* out, const BNW& bn) {
+  Op op;
+  op.kind = OP_POOL;
+  op.type = 2;
+  op.src = x.p; op.N = x.N; op.H = x.H; op.W = x.W; op.C = x.C;
+  op.mean = (const float*)bn.mean->p;
+  op.inv = (const float*)bn.inv->p;
+  op.out = out;
+  op.bytes = (double)es_of(B.m) * x.N * x.H * x.W * x.C + 4.0 * x.N * x.W * 2 * x.C;
+  B.ops->push_back(op);
+}
+
+static void emit_head(Builder& B, const float* pooled, int n, float* out) {
+  vox_model* m = B.m;
+  const ConvW& hw = m->head;
+  const int D = hw.cin;
+  // split-K: aim for ~512 blocks of 64 rows x 128 couts
+  const int gx = (n + 63) / 64, gy = hw.coutp / (16 * hw.wco);
+  int S = std::max(1, std::min(64, 512 / std::max(1, gx * gy)));
+  int kchunk = (hw.cinp + S - 1) / S;
+  kchunk = (kchunk + 15) / 16 * 16;
+  S = (hw.cinp + kchunk - 1) / kchunk;
+  float* part = (float*)B.base(S_PART, (size_t)S * n * hw.coutp * 4);
+  Op op;
+  op.kind = OP_HEAD;
+  op.type = 0;
+  ConvParams& p = op.cp;
+  std::memset(&p, 0, sizeof(p));
+  p.x = pooled; p.ldx = D;
+  p.w = hw.w->p; p.kp = hw.kp;
+  p.partial = part;
+  p.N = n; p.H = 1; p.W = 1; p.Cin = D; p.Ho = 1; p.Wo = 1; p.Cout = hw.cout; p.coutp = hw.coutp;
+  p.kh = 1; p.kw = 1; p.sh = p.sw = p.dh = p.dw = 1;
+  p.cinp = hw.cinp; p.kchunk = kchunk; p.flags = EPI_PARTIAL; p.ysplit = 1 << 30;
+  p.groups = 1; p.cblocks = gy;
+  op.cl.wco = hw.wco; op.cl.wpx = 1; op.cl.vec = 1; op.cl.splitk = S;
+  op.flops = 2.0 * n * D * hw.cout;
+  op.bytes = 4.0 * ((double)n * D + (double)D * hw.cout);
+  op.cp.fast4 = 0;
+  // dtype of the head is always fp32: mark with type 5 (fp32 conv)
+  op.type = 5;
+  B.ops->push_back(op);
+  Op r;
+  r.kind = OP_HEAD;
+  r.type = 1;
+  r.part = part; r.S = S; r.M = n; r.coutp = hw.coutp; r.cout = hw.cout;
+  r.flags = EPI_AFFINE;
+  r.mean = (const float*)hw.mean->p; r.inv = (const float*)hw.inv->p;
+  r.out = out; r.ldo = hw.cout;
+  r.bytes = 4.0 * ((double)S * n * hw.cout + (double)n * hw.cout);
+  B.ops->push_back(r);
+}
+
+static const void* emit_input(Builder& B, const float* x, int64_t count) {
+  vox_model* m = B.m;
+  if (m->dt == F32) return x;
+  void* in = B.base(S_IN, (size_t)count * 2);
+  Op op;
+  op.kind = OP_OTHER;
+  op.type = 4;
+  op.src = x; op.dst = in; op.count = count;
+  op.bytes = 6.0 * count;
+  B.ops->push_back(op);
+  return in;
+}
+
+static int build_tdnn(Builder& B, const float* x, int n, int t, float* out) {
+  vox_model* m = B.m;
+  const int F = m->feat_dim;
+  const size_t es = es_of(m);
+  auto kern = m->spec.getv("kernels");
+  auto dil = m->spec.getv("dilations");
+  Act a{emit_input(B, x, (int64_t)n * t * F), F, n, t, 1, F};
+  Slot ping[2] = {S_X0, S_X1};
+  for (size_t l = 0; l < m->convs.size(); ++l) {
+    const ConvW& cw = m->convs[l];
+    const int d = dil[l];
+    const int ph = ((kern[l] - 1) * d) / 2;  // SAME, stride 1 (Appendix A.2)
+    void* y = B.base(ping[l & 1], (size_t)n * t * cw.cout * es);
+    emit_conv(B, cw, a, nullptr, 0, 1, 1, d, 1, ph, 0, t, 1, y, cw.cout,
+              EPI_PRE_RELU | EPI_AFFINE);
+    a = Act{y, cw.cout, n, t, 1, cw.cout};
+  }
+  float* pooled = (float*)B.base(S_POOL, (size_t)n * 2 * a.C * 4);
+  emit_pool(B, a, pooled, m->head_bn1);
+  emit_head(B, pooled, n, out);
+  return VOX_OK;
+}
+
+static int build_res2net(Builder& B, const float* x, int n, int t, float* out) {
+  vox_model* m = B.m;
+  const size_t es = es_of(m);
+  const int s = m->spec.geti("split");
+  auto blocks = m->spec.getv("block_sizes");
+  auto strides = m->spec.getv("block_strides");
+  auto widths = m->spec.getv("widths");
+  int H = t, W = m->feat_dim;
+  Act in{emit_input(B, x, (int64_t)n * t * W), 1, n, H, W, 1};
+  size_t ci = 0;
+  const ConvW& stem = m->convs[ci++];
+  Slot cur_s = S_X0, nxt_s = S_X1;
+  void* y = B.base(cur_s, (size_t)n * H * W * stem.cout * es);
+  emit_conv(B, stem, in, nullptr, 0, 1, 1, 1, 1, 1, 1, H, W, y, stem.cout,
+            EPI_AFFINE | EPI_RELU);  // res2net_model.py:192-203, SAME pad 1
+  Act cur{y, stem.cout, n, H, W, stem.cout};
+  for (size_t st = 0; st < blocks.size(); ++st) {
+    const int w = widths[st];
+    const int sw = s * w;
+    for (int b = 0; b < blocks[st]; ++b) {
+      const int stride = b == 0 ? strides[st] : 1;
+      const int Ho = (H + stride - 1) / stride, Wo = (W + stride - 1) / stride;
+      const void* shortcut = cur.p;
+      int ld_sc = cur.ld;
+      if (b == 0) {  // projection_shortcut: 1x1 stride s, no pad, + BN (:85-87,125-127)
+        const ConvW& pr = m->convs[ci++];
+        void* sc = B.base(S_SC, (size_t)n * Ho * Wo * pr.cout * es);
+        emit_conv(B, pr, cur, nullptr, 0, stride, stride, 1, 1, 0, 0, Ho, Wo, sc, pr.cout,
+                  EPI_AFFINE);
+        shortcut = sc;
+        ld_sc = pr.cout;
+      }
+      const ConvW& c1a = m->convs[ci++];
+      char* A = B.base(S_A, (size_t)n * H * W * sw * es);
+      char* Bc = B.base(S_B, (size_t)n * Ho * Wo * sw * es);
+      if (stride == 1) {
+        // x_{s-1} passes straight through: write it into the concat buffer
+        emit_conv(B, c1a, cur, nullptr, 0, 1, 1, 1, 1, 0, 0, H, W, A, sw, EPI_AFFINE | EPI_RELU,
+                  nullptr, 0, Bc ? Bc + (size_t)(s - 1) * w * es : nullptr, sw, (s - 1) * w);
+      } else {
+        emit_conv(B, c1a, cur, nullptr, 0, 1, 1, 1, 1, 0, 0, H, W, A, sw, EPI_AFFINE | EPI_RELU);
+      }
+      for (int j = 0; j < s - 1; ++j) {  // res2net_pad_conv_bn_relu :53-75
+        const ConvW& br = m->convs[ci++];
+        Act xin{A ? A + (size_t)j * w * es : nullptr, sw, n, H, W, w};
+        const void* add = (stride == 1 && j > 0 && Bc) ? Bc + (size_t)(j - 1) * w * es : nullptr;
+        void* yb = Bc ? Bc + (size_t)j * w * es : nullptr;
+        // stride 1: SAME (pad 1); stride 2: fixed pad 1 + VALID -> same index map
+        emit_conv(B, br, xin, add, sw, stride, stride, 1, 1, 1, 1, Ho, Wo, yb, sw,
+                  EPI_AFFINE | EPI_RELU);
+      }
+      if (stride != 1) {  // last split: AvgPool 3x3/2 VALID on the padded tensor (:77)
+        Op op;
+        op.kind = OP_OTHER;
+        op.type = 3;
+        op.src = A ? A + (size_t)(s - 1) * w * es : nullptr;
+        op.lds = sw; op.N = n; op.H = H; op.W = W; op.C = w;
+        op.dst = Bc ? Bc + (size_t)(s - 1) * w * es : nullptr;
+        op.ldd = sw; op.Ho = Ho; op.Wo = Wo;
+        op.bytes = (double)es * ((double)n * H * W * w + (double)n * Ho * Wo * w);
+        B.ops->push_back(op);
+      }
+      const ConvW& c1c = m->convs[ci++];
+      void* yo = B.base(nxt_s, (size_t)n * Ho * Wo * c1c.cout * es);
+      Act bin{Bc, sw, n, Ho, Wo, sw};
+      emit_conv(B, c1c, bin, nullptr, 0, 1, 1, 1, 1, 0, 0, Ho, Wo, yo, c1c.cout,
+                EPI_AFFINE | EPI_RES | EPI_RELU, shortcut, ld_sc);  // :98-101
+      cur = Act{yo, c1c.cout, n, Ho, Wo, c1c.cout};
+      std::swap(cur_s, nxt_s);
+      H = Ho;
+      W = Wo;
+    }
+  }
+  float* pooled = (float*)B.base(S_POOL, (size_t)n * W * 2 * cur.C * 4);
+  emit_pool(B, cur, pooled, m->head_bn1);
+  emit_head(B, pooled, n, out);
+  return VOX_OK;
+}
+
+static int tf_same_beg(int n, int k, int s) {
+  const int out = (n + s - 1) / s;
+  const int total = std::max((out - 1) * s + k - n, 0);
+  return total / 2;
+}
+
+static int build_dpn(Builder& B, const float* x, int n, int t, float* out) {
+  vox_model* m = B.m;
+  const size_t es = es_of(m);
+  const int bw0 = m->spec.geti("bw"), kr = m->spec.geti("k_r");
+  auto ksec = m->spec.getv("k_sec");
+  auto inc_sec = m->spec.getv("inc_sec");
+  int H = t, W = m->feat_dim;
+  Act in{emit_input(B, x, (int64_t)n * t * W), 1, n, H, W, 1};
+  size_t ci = 0, bi = 0;
+  const ConvW& stem = m->convs[ci++];
+  Slot stage_s[2] = {S_X0, S_X1};
+  void* y = B.base(S_SC, (size_t)n * H * W * stem.cout * es);
+  emit_conv(B, stem, in, nullptr, 0, 1, 1, 1, 1, 1, 1, H, W, y, stem.cout,
+            EPI_AFFINE | EPI_RELU);  // conv_bn_relu, SAME
+  Act cur{y, stem.cout, n, H, W, stem.cout};
+  for (size_t st = 0; st < ksec.size(); ++st) {
+    const int bw = bw0 << st;
+    const int r = kr * bw / bw0;
+    const int inc = inc_sec[st];
+    const int blocks = ksec[st];
+    const int ctot = bw + 2 * inc + blocks * inc;  // final concat width of this stage
+    const int stride = st == 0 ? 1 : 2;
+    const int Ho = (H + stride - 1) / stride, Wo = (W + stride - 1) / stride;
+    char* S = B.base(stage_s[st & 1], (size_t)n * Ho * Wo * ctot * es);
+    int dense = 0;
+    for (int b = 0; b < blocks; ++b) {
+      const int bs = b == 0 ? stride : 1;
+      Act inp = cur;  // concat of [res | dense] = channel prefix of the stage buffer
+      if (b == 0) {  // projection: BN->ReLU->1x1 stride s -> [res bw | dense 2inc]
+        const BNW& pb = m->bns[bi++];
+        const ConvW& pc = m->convs[ci++];
+        emit_conv(B, pc, inp, nullptr, 0, bs, bs, 1, 1, tf_same_beg(H, 1, bs),
+                  tf_same_beg(W, 1, bs), Ho, Wo, S, ctot, 0, nullptr, 0, nullptr, 0, 1 << 30,
+                  (const float*)pb.mean->p, (const float*)pb.inv->p);
+        dense = 2 * inc;
+      } else {
+        inp = Act{S, ctot, n, Ho, Wo, bw + dense};
+      }
+      const int Hi = inp.H, Wi = inp.W;
+      // 1x1a
+      const BNW& b1 = m->bns[bi++];
+      const ConvW& c1 = m->convs[ci++];
+      char* A = B.base(S_A, (size_t)n * Hi * Wi * r * es);
+      emit_conv(B, c1, inp, nullptr, 0, 1, 1, 1, 1, 0, 0, Hi, Wi, A, r, 0, nullptr, 0, nullptr, 0,
+                1 << 30, (const float*)b1.mean->p, (const float*)b1.inv->p);
+      // grouped 3x3, stride bs, TF SAME (asymmetric for stride 2)
+      const BNW& b2 = m->bns[bi++];
+      const ConvW& c2 = m->convs[ci++];
+      char* Bb = B.base(S_B, (size_t)n * Ho * Wo * r * es);
+      emit_conv(B, c2, Act{A, r, n, Hi, Wi, r}, nullptr, 0, bs, bs, 1, 1, tf_same_beg(Hi, 3, bs),
+                tf_same_beg(Wi, 3, bs), Ho, Wo, Bb, r, 0, nullptr, 0, nullptr, 0, 1 << 30,
+                (const float*)b2.mean->p, (const float*)b2.inv->p);
+      // 1x1c -> [res add in place | new dense channels appended]
+      const BNW& b3 = m->bns[bi++];
+      const ConvW& c3 = m->convs[ci++];
+      emit_conv(B, c3, Act{Bb, r, n, Ho, Wo, r}, nullptr, 0, 1, 1, 1, 1, 0, 0, Ho, Wo, S, ctot,
+                EPI_RES, S, ctot, S ? S + (size_t)(bw + dense) * es : nullptr, ctot, bw,
+                (const float*)b3.mean->p, (const float*)b3.inv->p);
+      dense += inc;
+    }
+    cur = Act{S, ctot, n, Ho, Wo, bw + dense};
+    H = Ho;
+    W = Wo;
+  }
+  // concat_bn_relu: a BN+ReLU pass, fused as a 1x1 identity is wasteful;
+  // apply it inside the pool via a dedicated BN-ReLU elementwise op.
+  const BNW& fb = m->bns[bi++];
+  {
+    Op op;
+    op.kind = OP_OTHER;
+    op.type = 6;  // in-place BN+ReLU over [n,H,W,C] with ld
+    op.dst = (void*)cur.p; op.ldd = cur.ld; op.N = n; op.H = H; op.W = W; op.C = cur.C;
+    op.mean = (const float*)fb.mean->p; op.inv = (const float*)fb.inv->p;
+    op.bytes = 2.0 * es * n * H * W * cur.C;
+    B.ops->push_back(op);
+  }
+  float* pooled = (float*)B.base(S_POOL, (size_t)n * W * 2 * cur.C * 4);
+  emit_pool(B, cur, pooled, m->head_bn1);
+  emit_head(B, pooled, n, out);
+  return VOX_OK;
+}
+
+static int build_plan(vox_model* m, const float* x, int n, int t, float* out) {
+  auto run = [&](bool dry) -> int {
+    Builder B{m, dry, &m->plan};
+    m->plan.clear();
+    if (m->family == "tdnn") return build_tdnn(B, x, n, t, out);
+    if (m->family == "res2net") return build_res2net(B, x, n, t, out);
+    if (m->family == "dpn") return build_dpn(B, x, n, t, out);
+    return fail(VOX_EINVAL, "unknown family");
+  };
+  int rc = run(true);
+  if (rc) return rc;
+  for (int s = 0; s < S_NSLOTS; ++s) HIPCHK(m->slots[s].ensure(m->slot_need[s]));
+  rc = run(false);
+  if (rc) return rc;
+  m->plan_n = n;
+  m->plan_t = t;
+  m->plan_x = x;
+  m->plan_out = out;
+  return VOX_OK;
+}
+
+static hipError_t run_op(vox_model* m, const Op& op, hipStream_t s) {
+  switch (op.type) {
+    case 0: return launch_conv(m->dt, op.cp, op.cl, s);
+    case 5: return launch_conv(F32, op.cp, op.cl, s);
+    case 1:
+      return launch_splitk_reduce(op.part, op.S, op.M, op.coutp, op.cout, op.mean, op.inv,
+                                  op.flags, op.out, op.ldo, s);
+    case 2: return launch_stats_pool(m->dt, op.src, op.N, op.H, op.W, op.C, op.mean, op.inv, op.out, s);
+    case 3:
+      return launch_avgpool3s2(m->dt, op.src, op.lds, op.N, op.H, op.W, op.C, op.dst, op.ldd, op.Ho,
+                               op.Wo, s);
+    case 4: return launch_convert_f32(m->dt, (const float*)op.src, op.dst, op.count, s);
+    case 6:
+      return launch_bnrelu_inplace(m->dt, op.dst, op.ldd, (int64_t)op.N * op.H * op.W, op.C,
+                                   op.mean, op.inv, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+static int check_shape(vox_model* m, int n, int t, int f) {
+  if (n <= 0 || t <= 0) return fail(VOX_EINVAL, "empty batch");
+  if (f != m->feat_dim)
+    return fail(VOX_EINVAL, "feature dim " + std::to_string(f) + " != model " +
+                                std::to_string(m->feat_dim));
+  return VOX_OK;
+}
+
+static int ensure_plan(vox_model* m, const float* d_x, int n, int t, float* d_out) {
+  if (m->plan_n == n && m->plan_t == t && m->plan_x == d_x && m->plan_out == d_out) return VOX_OK;
+  return build_plan(m, d_x, n, t, d_out);
+}
+
+// ------------------------------------------------------------------ C-ABI
+extern "C" int vox_load_blob(const void* blob, size_t nbytes, int device, int precision,
+                             vox_model** out) {
+  if (!blob || !out) return fail(VOX_EINVAL, "null argument");
+  if (precision != VOX_FP32 && precision != VOX_BF16) return fail(VOX_EINVAL, "bad precision");
+  Spec spec;
+  std::vector<HostTensor> ts;
+  int rc = parse_blob((const uint8_t*)blob, nbytes, spec, ts);
+  if (rc) return rc;
+  int ndev = 0;
+  HIPCHK(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) return fail(VOX_EINVAL, "bad device index");
+  HIPCHK(hipSetDevice(device));
+  std::unique_ptr<vox_model> m(new vox_model());
+  m->device = device;
+  m->dt = precision == VOX_BF16 ? BF16 : F32;
+  m->spec = spec;
+  m->family = spec.get("family");
+  m->feat_dim = spec.geti("feat_dim");
+  m->expand_dim = spec.geti("expand_dim", 3);
+  if ((rc = load_weights(m.get(), ts))) return rc;
+  HIPCHK(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking));
+  *out = m.release();
+  return VOX_OK;
+}
+
+extern "C" int vox_load(const char* path, int device, int precision, vox_model** out) {
+  if (!path) return fail(VOX_EINVAL, "null path");
+  std::ifstream f(path, std::ios::binary);
+  if (!f) return fail(VOX_EIO, std::string("cannot open ") + path);
+  std::vector<char> raw((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+  return vox_load_blob(raw.data(), raw.size(), device, precision, out);
+}
+
+extern "C" void vox_free(vox_model* m) {
+  if (!m) return;
+  (void)hipSetDevice(m->device);
+  if (m->stream) {
+    (void)hipStreamSynchronize(m->stream);
+    (void)hipStreamDestroy(m->stream);
+  }
+  delete m;
+}
+
+extern "C" int vox_dim(const vox_model* m) { return m ? m->out_dim : VOX_EINVAL; }
+extern "C" int vox_feat_dim(const vox_model* m) { return m ? m->feat_dim : VOX_EINVAL; }
+extern "C" int vox_expand_dim(const vox_model* m) { return m ? m->expand_dim : VOX_EINVAL; }
+extern "C" int vox_precision(const vox_model* m) {
+  return m ? (m->dt == BF16 ? VOX_BF16 : VOX_FP32) : VOX_EINVAL;
+}
+
+extern "C" int vox_embed_device(vox_model* m, const float* d_x, int n, int t, int f, float* d_out,
+                                void* stream) {
+  if (!m || !d_x || !d_out) return fail(VOX_EINVAL, "null argument");
+  int rc = check_shape(m, n, t, f);
+  if (rc) return rc;
+  HIPCHK(hipSetDevice(m->device));
+  if ((rc = ensure_plan(m, d_x, n, t, d_out))) return rc;
+  hipStream_t s = stream ? (hipStream_t)stream : m->stream;
+  for (const Op& op : m->plan) HIPCHK(run_op(m, op, s));
+  return VOX_OK;
+}
+
+extern "C" int vox_embed(vox_model* m, const float* x, int n, int t, int f, float* out) {
+  if (!m || !x || !out) return fail(VOX_EINVAL, "null argument");
+  int rc = check_shape(m, n, t, f);
+  if (rc) return rc;
+  HIPCHK(hipSetDevice(m->device));
+  const size_t in_b = (size_t)n * t * f * 4, out_b = (size_t)n * m->out_dim * 4;
+  HIPCHK(m->stage_in.ensure(in_b));
+  HIPCHK(m->stage_out.ensure(out_b));
+  HIPCHK(hipMemcpyAsync(m->stage_in.p, x, in_b, hipMemcpyHostToDevice, m->stream));
+  rc = vox_embed_device(m, (const float*)m->stage_in.p, n, t, f, (float*)m->stage_out.p, m->stream);
+  if (rc) return rc;
+  HIPCHK(hipMemcpyAsync(out, m->stage_out.p, out_b, hipMemcpyDeviceToHost, m->stream));
+  HIPCHK(hipStreamSynchronize(m->stream));
+  return VOX_OK;
+}
+
+extern "C" int vox_embed_utt(vox_model* m, const float* x, int t, int f, float* out) {
+  if (!m || !x || !out) return fail(VOX_EINVAL, "null argument");
+  const int max_frames = 1000;
+  if (t < 25)  // tf_extract.py:102 -> 0 chunks -> ZeroDivisionError at :111
+    return fail(VOX_ESHORT, "utterance shorter than 25 frames (reference: ZeroDivisionError)");
+  const int nchunks = 1 + (t - 25) / max_frames;
+  const int D = m->out_dim;
+  std::vector<float> acc(D, 0.f), e(D);
+  int total = 0;
+  for (int i = 0; i < nchunks; ++i) {
+    const int len = (i + 1) * max_frames <= t ? max_frames : t - i * max_frames;
+    int rc = vox_embed(m, x + (size_t)i * max_frames * f, 1, len, f, e.data());
+    if (rc) return rc;
+    for (int d = 0; d < D; ++d) acc[d] += e[d] * (float)len;  // target_value * input_length
+    total += len;
+  }
+  for (int d = 0; d < D; ++d) out[d] = acc[d] / (float)total;
+  return VOX_OK;
+}
+
+extern "C" int vox_profile(vox_model* m, const float* d_x, int n, int t, int f, int reps,
+                           float* op_ms, double* op_flops, double* op_bytes, int* op_kind,
+                           int max_ops, void* stream) {
+  if (!m || !d_x) return fail(VOX_EINVAL, "null argument");
+  int rc = check_shape(m, n, t, f);
+  if (rc) return rc;
+  HIPCHK(hipSetDevice(m->device));
+  HIPCHK(m->stage_out.ensure((size_t)n * m->out_dim * 4));
+  float* d_out = (float*)m->stage_out.p;
+  if ((rc = ensure_plan(m, d_x, n, t, d_out))) return rc;
+  hipStream_t s = stream ? (hipStream_t)stream : m->stream;
+  const int nops = (int)m->plan.size();
+  std::vector<hipEvent_t> ev(nops + 1);
+  for (auto& e : ev) HIPCHK(hipEventCreate(&e));
+  std::vector<double> tot(nops, 0.0);
+  for (int r = 0; r < std::max(1, reps); ++r) {
+    HIPCHK(hipEventRecord(ev[0], s));
+    for (int i = 0; i < nops; ++i) {
+      HIPCHK(run_op(m, m->plan[i], s));
+      HIPCHK(hipEventRecord(ev[i + 1], s));
+    }
+    HIPCHK(hipEventSynchronize(ev[nops]));
+    for (int i = 0; i < nops; ++i) {
+      float ms = 0.f;
+      HIPCHK(hipEventElapsedTime(&ms, ev[i], ev[i + 1]));
+      tot[i] += ms;
+    }
+  }
+  for (auto& e : ev) (void)hipEventDestroy(e);
+  for (int i = 0; i < nops && i < max_ops; ++i) {
+    if (op_ms) op_ms[i] = (float)(tot[i] / std::max(1, reps));
+    if (op_flops) op_flops[i] = m->plan[i].flops;
+    if (op_bytes) op_bytes[i] = m->plan[i].bytes;
+    if (op_kind) {
+      // kind | kernel-variant tag (wco, wpx, vec, fp32) so callers can group
+      // launches by template instantiation, as rocprof names them
+      const Op& o = m->plan[i];
+      int tag = o.kind;
+      if (o.type == 0 || o.type == 5)
+        tag |= (o.cl.wco << 4) | (o.cl.wpx << 8) | (o.cl.vec << 12) |
+               ((o.type == 5 || m->dt == F32) ? 1 << 13 : 0) | (1 << 14);
+      op_kind[i] = tag;
+    }
+  }
+  return nops;
+}
+
+extern "C" int vox_stats_pool_device(const void* d_x, int dtype, int n, int h, int w, int c,
+                                     const float* d_mean, const float* d_inv, float* d_out,
+                                     void* stream) {
+  if (!d_x || !d_out || n <= 0 || h <= 0 || w <= 0 || c <= 0)
+    return fail(VOX_EINVAL, "bad stats-pool arguments");
+  if (dtype != VOX_FP32 && dtype != VOX_BF16) return fail(VOX_EINVAL, "bad dtype");
+  HIPCHK(launch_stats_pool(dtype == VOX_BF16 ? BF16 : F32, d_x, n, h, w, c, d_mean, d_inv, d_out,
+                           (hipStream_t)stream));
+  return VOX_OK;
+}

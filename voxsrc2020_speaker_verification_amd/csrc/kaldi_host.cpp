@@ -1,0 +1,259 @@
+// Host-side Kaldi table I/O and sliding CMN -- the parts of the reference's
+// read/write path that live in Kaldi binaries or kaldi_io.py:
+//   * apply-cmvn-sliding --norm-vars=false --center=true --cmn-window=300
+//     (tensorflow/tf_extract.py:63), restated from Kaldi's
+//     SlidingWindowCmnInternal: double-precision running sums, window
+//     [t-w/2, t-w/2+w) shifted to stay inside [0,T), output = x - sum/n.
+//   * binary matrix reader "\0B" + FM / DM / CM (kaldi_io.py:420-454), with
+//     CM decoded exactly as kaldi_io._read_compressed_mat (kaldi_io.py:471-504,
+//     float32 arithmetic in the same operation order).
+//   * FV record writer (kaldi_io.write_vec_flt, kaldi_io.py:304-334).
+// Compiled with -ffp-contract=off so no multiply-add is fused.
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/voxemb.h"
+
+int vox_set_error(int code, const char* msg);  // api.cpp (shared thread-local message)
+static int kfail(int code, const char* msg) { return vox_set_error(code, msg); }
+
+extern "C" int vox_sliding_cmn(const float* in, int T, int F, int cmn_window, int center,
+                               float* out) {
+  if (!in || !out || T <= 0 || F <= 0 || cmn_window <= 0) return kfail(VOX_EINVAL, "bad cmn args");
+  const int min_window = 100;  // Kaldi default (only used when center == false)
+  std::vector<double> sum(F, 0.0);
+  int last_start = -1, last_end = -1;
+  for (int t = 0; t < T; ++t) {
+    int ws, we;
+    if (center) {
+      ws = t - cmn_window / 2;
+      we = ws + cmn_window;
+    } else {
+      ws = t - cmn_window;
+      we = t + 1;
+    }
+    if (ws < 0) {
+      we -= ws;
+      ws = 0;
+    }
+    if (!center && we < min_window) we = min_window;
+    if (we > T) {
+      ws -= (we - T);
+      we = T;
+      if (ws < 0) ws = 0;
+    }
+    if (last_start == -1) {
+      for (int r = ws; r < we; ++r)
+        for (int f = 0; f < F; ++f) sum[f] += (double)in[(size_t)r * F + f];
+    } else {
+      if (ws > last_start)
+        for (int f = 0; f < F; ++f) sum[f] -= (double)in[(size_t)last_start * F + f];
+      if (we > last_end)
+        for (int f = 0; f < F; ++f) sum[f] += (double)in[(size_t)last_end * F + f];
+    }
+    const int n = we - ws;
+    last_start = ws;
+    last_end = we;
+    const double alpha = -1.0 / n;
+    for (int f = 0; f < F; ++f)
+      out[(size_t)t * F + f] = (float)((double)in[(size_t)t * F + f] + alpha * sum[f]);
+  }
+  return VOX_OK;
+}
+
+// ---------------------------------------------------------------- matrices
+namespace {
+struct Reader {
+  const uint8_t* p;
+  size_t n, i = 0;
+  bool take(void* dst, size_t k) {
+    if (i + k > n) return false;
+    std::memcpy(dst, p + i, k);
+    i += k;
+    return true;
+  }
+};
+
+// Parse the header; on success sets rows/cols/kind and leaves r at the payload.
+int parse_header(Reader& r, int* rows, int* cols, int* kind /*0 FM 1 DM 2 CM*/) {
+  char b[2];
+  if (!r.take(b, 2)) return kfail(VOX_EIO, "truncated matrix");
+  if (b[0] != '\0' || b[1] != 'B') return kfail(VOX_EIO, "not a binary Kaldi matrix (ascii unsupported)");
+  char h[3];
+  if (!r.take(h, 3)) return kfail(VOX_EIO, "truncated matrix header");
+  if (h[0] == 'C' && h[1] == 'M') {
+    if (h[2] != ' ') return kfail(VOX_EIO, "CM2/CM3 compressed formats are not supported");
+    float mn, range;
+    int32_t nr, nc;
+    if (!r.take(&mn, 4) || !r.take(&range, 4) || !r.take(&nr, 4) || !r.take(&nc, 4))
+      return kfail(VOX_EIO, "truncated CM header");
+    *rows = nr;
+    *cols = nc;
+    *kind = 2;
+    return VOX_OK;
+  }
+  if (h[0] == 'F' && h[1] == 'M' && h[2] == ' ') *kind = 0;
+  else if (h[0] == 'D' && h[1] == 'M' && h[2] == ' ') *kind = 1;
+  else return kfail(VOX_EIO, "unknown matrix header");
+  int8_t s1, s2;
+  int32_t nr, nc;
+  if (!r.take(&s1, 1) || !r.take(&nr, 4) || !r.take(&s2, 1) || !r.take(&nc, 4))
+    return kfail(VOX_EIO, "truncated matrix dims");
+  if (nr < 0 || nc < 0) return kfail(VOX_EIO, "negative matrix dims");
+  *rows = nr;
+  *cols = nc;
+  return VOX_OK;
+}
+
+int parse_payload(Reader& r, int kind, int rows, int cols, float* out) {
+  const size_t n = (size_t)rows * cols;
+  if (kind == 0) {
+    if (!r.take(out, n * 4)) return kfail(VOX_EIO, "truncated FM payload");
+    return VOX_OK;
+  }
+  if (kind == 1) {
+    std::vector<double> d(n);
+    if (!r.take(d.data(), n * 8)) return kfail(VOX_EIO, "truncated DM payload");
+    for (size_t i = 0; i < n; ++i) out[i] = (float)d[i];
+    return VOX_OK;
+  }
+  // CM: re-read the global header fields that precede the column headers
+  float mn, range;
+  std::memcpy(&mn, r.p + r.i - 16, 4);
+  std::memcpy(&range, r.p + r.i - 12, 4);
+  std::vector<uint16_t> ch((size_t)cols * 4);
+  if (!r.take(ch.data(), ch.size() * 2)) return kfail(VOX_EIO, "truncated CM column headers");
+  std::vector<uint8_t> data(n);
+  if (!r.take(data.data(), n)) return kfail(VOX_EIO, "truncated CM payload");
+  const float c = 1.52590218966964e-05f;
+  for (int col = 0; col < cols; ++col) {
+    float p[4];
+    for (int k = 0; k < 4; ++k) {
+      // kaldi_io: uint16 * float32(range) * float32(1/65535) + float32(min), float32 ops
+      float v = (float)ch[(size_t)col * 4 + k] * range;
+      v = v * c;
+      p[k] = v + mn;
+    }
+    const float s0 = (p[1] - p[0]) / 64.0f;
+    const float s1 = (p[2] - p[1]) / 128.0f;
+    const float s2 = (p[3] - p[2]) / 63.0f;
+    const uint8_t* d = &data[(size_t)col * rows];  // column-major
+    for (int row = 0; row < rows; ++row) {
+      const unsigned v = d[row];
+      float x;
+      if (v <= 64) x = p[0] + s0 * (float)v;
+      else if (v <= 192) x = p[1] + s1 * (float)(v - 64);
+      else x = p[2] + s2 * (float)(v - 192);
+      out[(size_t)row * cols + col] = x;
+    }
+  }
+  return VOX_OK;
+}
+
+int read_file_at(const char* path, int64_t offset, std::vector<uint8_t>& buf) {
+  FILE* f = std::fopen(path, "rb");
+  if (!f) return kfail(VOX_EIO, "cannot open matrix file");
+  if (std::fseek(f, 0, SEEK_END) != 0) {
+    std::fclose(f);
+    return kfail(VOX_EIO, "seek failed");
+  }
+  const long size = std::ftell(f);
+  if (offset < 0 || offset > size) {
+    std::fclose(f);
+    return kfail(VOX_EIO, "offset beyond end of file");
+  }
+  // read the header first to size the payload
+  std::fseek(f, (long)offset, SEEK_SET);
+  const size_t head = std::min<size_t>(64, (size_t)(size - offset));
+  buf.resize(head);
+  if (std::fread(buf.data(), 1, head, f) != head) {
+    std::fclose(f);
+    return kfail(VOX_EIO, "short read");
+  }
+  Reader r{buf.data(), buf.size()};
+  int rows, cols, kind;
+  int rc = parse_header(r, &rows, &cols, &kind);
+  if (rc) {
+    std::fclose(f);
+    return rc;
+  }
+  size_t total = r.i;
+  if (kind == 0) total += (size_t)rows * cols * 4;
+  else if (kind == 1) total += (size_t)rows * cols * 8;
+  else total += (size_t)cols * 8 + (size_t)rows * cols;
+  if ((size_t)offset + total > (size_t)size) {
+    std::fclose(f);
+    return kfail(VOX_EIO, "matrix extends beyond end of file");
+  }
+  buf.resize(total);
+  std::fseek(f, (long)offset, SEEK_SET);
+  const size_t got = std::fread(buf.data(), 1, total, f);
+  std::fclose(f);
+  if (got != total) return kfail(VOX_EIO, "short read");
+  return VOX_OK;
+}
+}  // namespace
+
+extern "C" int vox_parse_mat_shape(const uint8_t* buf, size_t nbytes, int* rows, int* cols) {
+  if (!buf || !rows || !cols) return kfail(VOX_EINVAL, "null argument");
+  Reader r{buf, nbytes};
+  int kind;
+  return parse_header(r, rows, cols, &kind);
+}
+
+extern "C" int vox_parse_mat(const uint8_t* buf, size_t nbytes, float* out, int rows, int cols,
+                             size_t* consumed) {
+  if (!buf || (!out && rows * cols > 0)) return kfail(VOX_EINVAL, "null argument");
+  Reader r{buf, nbytes};
+  int nr, nc, kind;
+  int rc = parse_header(r, &nr, &nc, &kind);
+  if (rc) return rc;
+  if (nr != rows || nc != cols) return kfail(VOX_EINVAL, "matrix shape mismatch");
+  rc = parse_payload(r, kind, nr, nc, out);
+  if (rc) return rc;
+  if (consumed) *consumed = r.i;
+  return VOX_OK;
+}
+
+extern "C" int vox_mat_shape(const char* path, int64_t offset, int* rows, int* cols) {
+  if (!path || !rows || !cols) return kfail(VOX_EINVAL, "null argument");
+  std::vector<uint8_t> buf;
+  int rc = read_file_at(path, offset, buf);
+  if (rc) return rc;
+  return vox_parse_mat_shape(buf.data(), buf.size(), rows, cols);
+}
+
+extern "C" int vox_read_mat(const char* path, int64_t offset, float* out, int rows, int cols) {
+  if (!path) return kfail(VOX_EINVAL, "null argument");
+  std::vector<uint8_t> buf;
+  int rc = read_file_at(path, offset, buf);
+  if (rc) return rc;
+  return vox_parse_mat(buf.data(), buf.size(), out, rows, cols, nullptr);
+}
+
+extern "C" int64_t vox_format_vec_flt(const char* key, const float* v, int dim, uint8_t* buf,
+                                      size_t cap, int64_t* data_offset) {
+  if (!key || dim < 0 || (!v && dim > 0)) return kfail(VOX_EINVAL, "bad arguments");
+  const size_t klen = std::strlen(key);
+  if (klen == 0 || std::strchr(key, ' ')) return kfail(VOX_EINVAL, "key must be non-empty without spaces");
+  const size_t need = klen + 1 + 2 + 3 + 1 + 4 + (size_t)dim * 4;
+  if (data_offset) *data_offset = (int64_t)klen + 1;
+  if (!buf || cap < need) return (int64_t)need;
+  uint8_t* q = buf;
+  std::memcpy(q, key, klen);
+  q += klen;
+  *q++ = ' ';
+  *q++ = '\0';
+  *q++ = 'B';
+  std::memcpy(q, "FV ", 3);
+  q += 3;
+  *q++ = 4;
+  const uint32_t d = (uint32_t)dim;
+  std::memcpy(q, &d, 4);
+  q += 4;
+  std::memcpy(q, v, (size_t)dim * 4);
+  return (int64_t)need;
+}

@@ -1,0 +1,68 @@
+// Internal kernel interface of libvoxemb (not part of the C-ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace vox {
+
+enum DType { F32 = 0, BF16 = 1 };
+
+// Epilogue flags, applied in this order:
+//   PRE_RELU  v = max(v,0)                (TDNN conv->ReLU->BN, tdnn_model.py:24-30)
+//   AFFINE    v = (v - mean[c]) * inv[c]  (inference BN, models.py:62-67)
+//   RES       v += res[p][c]              (residual, res2net_model.py:100), only c < ysplit
+//   RELU      v = max(v,0)
+//   PARTIAL   raw accumulator -> split-K slab (no other flag applies)
+enum EpiFlags { EPI_PRE_RELU = 1, EPI_AFFINE = 2, EPI_RES = 4, EPI_RELU = 8, EPI_PARTIAL = 16 };
+
+// NHWC implicit-GEMM convolution, C[cout][pixel] = W[cout][k] * im2col[k][pixel].
+struct ConvParams {
+  const void* x;  int ldx;                 // input, channel stride (elements)
+  const void* x2; int ldx2;                // optional addend of identical geometry
+  const float* in_mean; const float* in_inv;  // optional prologue relu((x-m)*inv)
+  const void* w;  int kp;                  // weights [coutp][kp]
+  void* y;  int ldy;                       // output (channel offset pre-applied)
+  void* y2; int ldy2; int ysplit;          // channels >= ysplit go to y2[c - ysplit]
+  const void* res; int ldr;                // residual
+  const float* mean; const float* inv;     // epilogue BN
+  float* partial;                          // split-K slabs [z][M][coutp]
+  int N, H, W, Cin, Ho, Wo, Cout, coutp;
+  int kh, kw, sh, sw, dh, dw, ph, pw;
+  int cinp;                                // per-tap padded Cin (vector path)
+  int kchunk;                              // split-K Cin range per blockIdx.z
+  int flags;
+  int fast4;                               // 4-channel vector epilogue allowed
+  int groups;                              // grouped conv (Cin/Cout are per group)
+  int cblocks;                             // cout blocks per group (gridDim.y = groups*cblocks)
+};
+
+struct ConvLaunch {
+  int wco, wpx;       // 16-row cout tiles / 16-pixel tiles per wave
+  int vec;            // 1: vector (tap-major, Cin % VEC == 0) path
+  int splitk;         // blockIdx.z count
+};
+
+// Returns hipSuccess or the launch error.
+hipError_t launch_conv(DType t, const ConvParams& p, const ConvLaunch& l, hipStream_t s);
+int conv_kstep(DType t);   // 32 (bf16) / 16 (fp32)
+int conv_vec(DType t);     // elements per 16-byte lane load: 8 / 4
+
+hipError_t launch_splitk_reduce(const float* partial, int S, int M, int coutp, int cout,
+                                const float* mean, const float* inv, int flags,
+                                float* out, int ldo, hipStream_t s);
+
+hipError_t launch_stats_pool(DType t, const void* x, int N, int H, int W, int C,
+                             const float* mean, const float* inv, float* out, hipStream_t s);
+
+hipError_t launch_avgpool3s2(DType t, const void* x, int ldx, int N, int H, int W, int C,
+                             void* y, int ldy, int Ho, int Wo, hipStream_t s);
+
+hipError_t launch_convert_f32(DType t, const float* x, void* y, int64_t n, hipStream_t s);
+
+hipError_t launch_copy_channels(DType t, const void* x, int ldx, void* y, int ldy,
+                                int64_t npix, int C, hipStream_t s);
+
+hipError_t launch_bnrelu_inplace(DType t, void* x, int ld, int64_t npix, int C, const float* mean,
+                                 const float* inv, hipStream_t s);
+
+}  // namespace vox

@@ -1,0 +1,587 @@
+// gfx950 (CDNA4) kernels of the embedding-extraction hot path.
+//
+//  * conv_igemm   -- NHWC implicit-GEMM convolution on MFMA (bf16 16x16x32 or
+//                    f32 16x16x4), BN/ReLU/residual epilogues, split outputs
+//                    (free channel concat), hierarchical-add and BN+ReLU
+//                    prologues, split-K partial slabs.  Replaces TF Conv2D +
+//                    FusedBatchNormV3 + Relu + AddV2 + Split/ConcatV2
+//                    (models.py:155-203, res2net_model.py:26-103,
+//                    tdnn_model.py:24-30, dpn_model.py:40-87).
+//  * stats_pool   -- wave-parallel mean/std over time + head BN
+//                    (models.py:262-269, res2net_model.py:239).
+//  * splitk_reduce-- deterministic fixed-order split-K combine + BN (head dense,
+//                    res2net_model.py:240-241).
+//  * avgpool3s2   -- AvgPool 3x3/2 VALID over the fixed-padded tensor, divisor 9
+//                    (res2net_model.py:27-28,77).
+#include "kernels.h"
+
+namespace vox {
+
+typedef __bf16 bf16_t;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <typename T> struct Tr;
+template <> struct Tr<bf16_t> {
+  static constexpr int VEC = 8;     // elements per 16-byte lane load
+  static constexpr int KSTEP = 32;  // K per MFMA step (16x16x32)
+  typedef bf16x8 frag;
+};
+template <> struct Tr<float> {
+  static constexpr int VEC = 4;
+  static constexpr int KSTEP = 16;  // 4 x mfma 16x16x4 over a permuted K
+  typedef f32x4 frag;
+};
+
+__device__ __forceinline__ bf16x8 ld16(const bf16_t* p) {
+  uint4 u = *reinterpret_cast<const uint4*>(p);
+  return __builtin_bit_cast(bf16x8, u);
+}
+__device__ __forceinline__ f32x4 ld16(const float* p) {
+  return *reinterpret_cast<const f32x4*>(p);
+}
+
+template <typename F> __device__ __forceinline__ F zero_frag() { return F{}; }
+
+// Elementwise helpers on fragments (in fp32).
+__device__ __forceinline__ bf16x8 frag_add(bf16x8 a, bf16x8 b) {
+  bf16x8 r;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) r[e] = (bf16_t)((float)a[e] + (float)b[e]);
+  return r;
+}
+__device__ __forceinline__ f32x4 frag_add(f32x4 a, f32x4 b) { return a + b; }
+
+__device__ __forceinline__ bf16x8 frag_bnrelu(bf16x8 a, const float* m, const float* iv) {
+  bf16x8 r;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) r[e] = (bf16_t)fmaxf(((float)a[e] - m[e]) * iv[e], 0.f);
+  return r;
+}
+__device__ __forceinline__ f32x4 frag_bnrelu(f32x4 a, const float* m, const float* iv) {
+  f32x4 r;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) r[e] = fmaxf((a[e] - m[e]) * iv[e], 0.f);
+  return r;
+}
+
+__device__ __forceinline__ f32x4 mfma_step(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+// f32: lane l holds k = 4*(l>>4)+j in element j of both operands; MFMA j uses
+// element j, i.e. internal k index kk <-> real k = 4*kk + j for A and B alike.
+__device__ __forceinline__ f32x4 mfma_step(f32x4 a, f32x4 b, f32x4 c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b[0], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], b[1], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], b[2], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], b[3], c, 0, 0, 0);
+  return c;
+}
+
+__device__ __forceinline__ void store4(bf16_t* p, const float* v) {
+  bf16x4 r;
+  r[0] = (bf16_t)v[0]; r[1] = (bf16_t)v[1]; r[2] = (bf16_t)v[2]; r[3] = (bf16_t)v[3];
+  *reinterpret_cast<bf16x4*>(p) = r;
+}
+__device__ __forceinline__ void store4(float* p, const float* v) {
+  *reinterpret_cast<f32x4*>(p) = f32x4{v[0], v[1], v[2], v[3]};
+}
+__device__ __forceinline__ void load4(const bf16_t* p, float* v) {
+  bf16x4 r = *reinterpret_cast<const bf16x4*>(p);
+  v[0] = (float)r[0]; v[1] = (float)r[1]; v[2] = (float)r[2]; v[3] = (float)r[3];
+}
+__device__ __forceinline__ void load4(const float* p, float* v) {
+  f32x4 r = *reinterpret_cast<const f32x4*>(p);
+  v[0] = r[0]; v[1] = r[1]; v[2] = r[2]; v[3] = r[3];
+}
+
+// ----------------------------------------------------------------------------
+// Implicit-GEMM conv.  MFMA rows = output channels (A = weights [coutp][kp]),
+// MFMA columns = output pixels (B = im2col, gathered straight from NHWC).
+// Block = 4 waves stacked along pixels; a wave owns WCO x WPX 16x16 tiles.
+// The accumulator layout (col = lane&15 = pixel, rows 4*(lane>>4)+r = couts)
+// gives every lane 4 consecutive channels of one pixel in the epilogue.
+template <typename T, int WCO, int WPX, bool VEC>
+__global__ __launch_bounds__(256) void conv_igemm(ConvParams p) {
+  typedef typename Tr<T>::frag frag;
+  constexpr int VN = Tr<T>::VEC;
+  constexpr int KS = Tr<T>::KSTEP;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int M = p.N * p.Ho * p.Wo;
+  const int HoWo = p.Ho * p.Wo;
+  const int grp = blockIdx.y / p.cblocks;
+  const int co0 = (blockIdx.y - grp * p.cblocks) * (16 * WCO);
+  const int pbase = (blockIdx.x * 4 + wave) * (16 * WPX);
+  if (pbase >= M) return;
+  const int col = lane & 15;
+  const int kl = (lane >> 4) * VN;
+
+  int pn[WPX], pho[WPX], pwo[WPX];
+  bool pv[WPX];
+#pragma unroll
+  for (int j = 0; j < WPX; ++j) {
+    int pix = pbase + 16 * j + col;
+    pv[j] = pix < M;
+    int q = pv[j] ? pix : 0;
+    pn[j] = q / HoWo;
+    int r = q - pn[j] * HoWo;
+    pho[j] = r / p.Wo;
+    pwo[j] = r - pho[j] * p.Wo;
+  }
+
+  f32x4 acc[WCO][WPX];
+#pragma unroll
+  for (int i = 0; i < WCO; ++i)
+#pragma unroll
+    for (int j = 0; j < WPX; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // grouped conv: per-group channel offsets (groups == 1 -> all zero)
+  const T* __restrict__ X = reinterpret_cast<const T*>(p.x) + grp * p.Cin;
+  const T* __restrict__ X2 = p.x2 ? reinterpret_cast<const T*>(p.x2) + grp * p.Cin : nullptr;
+  const float* in_mean = p.in_mean ? p.in_mean + grp * p.Cin : nullptr;
+  const float* in_inv = p.in_inv ? p.in_inv + grp * p.Cin : nullptr;
+  const T* __restrict__ Wt = reinterpret_cast<const T*>(p.w) + (size_t)grp * p.coutp * p.kp;
+  const T* wrow[WCO];
+#pragma unroll
+  for (int i = 0; i < WCO; ++i) wrow[i] = Wt + (size_t)(co0 + 16 * i + col) * p.kp;
+
+  if constexpr (VEC) {
+    const int taps = p.kh * p.kw;
+    int cbeg = 0, cend = p.cinp;
+    if (gridDim.z > 1) {
+      cbeg = blockIdx.z * p.kchunk;
+      cend = min(cbeg + p.kchunk, p.cinp);
+    }
+    for (int tap = 0; tap < taps; ++tap) {
+      const int ky = tap / p.kw, kx = tap - (tap / p.kw) * p.kw;
+      const T* xb[WPX];
+      const T* xb2[WPX];
+#pragma unroll
+      for (int j = 0; j < WPX; ++j) {
+        int hi = pho[j] * p.sh - p.ph + ky * p.dh;
+        int wi = pwo[j] * p.sw - p.pw + kx * p.dw;
+        bool ok = pv[j] && hi >= 0 && hi < p.H && wi >= 0 && wi < p.W;
+        size_t pix = ((size_t)pn[j] * p.H + hi) * p.W + wi;
+        xb[j] = ok ? X + pix * p.ldx : nullptr;
+        xb2[j] = (ok && X2) ? X2 + pix * p.ldx2 : nullptr;
+      }
+      const int woff = tap * p.cinp;
+      for (int c0 = cbeg; c0 < cend; c0 += KS) {
+        const int c = c0 + kl;
+        frag a[WCO], b[WPX];
+#pragma unroll
+        for (int i = 0; i < WCO; ++i) a[i] = ld16(wrow[i] + woff + c);
+        const bool cin_ok = c < p.Cin;
+        float im[VN], ii[VN];
+        if (in_mean && cin_ok) {
+#pragma unroll
+          for (int e = 0; e < VN; ++e) { im[e] = in_mean[c + e]; ii[e] = in_inv[c + e]; }
+        }
+#pragma unroll
+        for (int j = 0; j < WPX; ++j) {
+          if (xb[j] && cin_ok) {
+            frag v = ld16(xb[j] + c);
+            if (xb2[j]) v = frag_add(v, ld16(xb2[j] + c));
+            if (in_mean) v = frag_bnrelu(v, im, ii);
+            b[j] = v;
+          } else {
+            b[j] = zero_frag<frag>();
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < WCO; ++i)
+#pragma unroll
+          for (int j = 0; j < WPX; ++j) acc[i][j] = mfma_step(a[i], b[j], acc[i][j]);
+      }
+    }
+  } else {
+    // Gather path (Cin not a multiple of VN, e.g. the 1-channel stem): K is
+    // flattened as k = tap*Cin + ci and padded to kp.
+    const int K = p.kh * p.kw * p.Cin;
+    for (int k0 = 0; k0 < p.kp; k0 += KS) {
+      frag a[WCO], b[WPX];
+#pragma unroll
+      for (int i = 0; i < WCO; ++i) a[i] = ld16(wrow[i] + k0 + kl);
+#pragma unroll
+      for (int j = 0; j < WPX; ++j) {
+        frag v;
+#pragma unroll
+        for (int e = 0; e < VN; ++e) {
+          int k = k0 + kl + e;
+          float val = 0.f;
+          if (pv[j] && k < K) {
+            int tap = k / p.Cin, ci = k - (k / p.Cin) * p.Cin;
+            int ky = tap / p.kw, kx = tap - (tap / p.kw) * p.kw;
+            int hi = pho[j] * p.sh - p.ph + ky * p.dh;
+            int wi = pwo[j] * p.sw - p.pw + kx * p.dw;
+            if (hi >= 0 && hi < p.H && wi >= 0 && wi < p.W) {
+              size_t pix = ((size_t)pn[j] * p.H + hi) * p.W + wi;
+              val = (float)X[pix * p.ldx + ci];
+              if (X2) val += (float)X2[pix * p.ldx2 + ci];
+              if (in_mean) val = fmaxf((val - in_mean[ci]) * in_inv[ci], 0.f);
+            }
+          }
+          v[e] = (T)val;
+        }
+        b[j] = v;
+      }
+#pragma unroll
+      for (int i = 0; i < WCO; ++i)
+#pragma unroll
+        for (int j = 0; j < WPX; ++j) acc[i][j] = mfma_step(a[i], b[j], acc[i][j]);
+    }
+  }
+
+  // ---------------------------------------------------------------- epilogue
+  const int goff = grp * p.Cout;
+  T* __restrict__ Y = reinterpret_cast<T*>(p.y) + goff;
+  T* __restrict__ Y2 = reinterpret_cast<T*>(p.y2);
+  const T* __restrict__ R = p.res ? reinterpret_cast<const T*>(p.res) + goff : nullptr;
+  const float* __restrict__ bnm = p.mean ? p.mean + goff : nullptr;
+  const float* __restrict__ bni = p.inv ? p.inv + goff : nullptr;
+  const int flags = p.flags;
+#pragma unroll
+  for (int i = 0; i < WCO; ++i) {
+    const int co = co0 + 16 * i + 4 * (lane >> 4);
+    if (co >= p.Cout) continue;
+#pragma unroll
+    for (int j = 0; j < WPX; ++j) {
+      if (!pv[j]) continue;
+      const size_t pix = (size_t)(pbase + 16 * j + col);
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if (flags & EPI_PARTIAL) {
+        float* dst = p.partial + ((size_t)blockIdx.z * M + pix) * p.coutp + co;
+        *reinterpret_cast<f32x4*>(dst) = f32x4{v[0], v[1], v[2], v[3]};
+        continue;
+      }
+      if (p.fast4 && co + 3 < p.Cout) {
+        if (flags & EPI_PRE_RELU) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+        }
+        if (flags & EPI_AFFINE) {
+          f32x4 m = *reinterpret_cast<const f32x4*>(bnm + co);
+          f32x4 s = *reinterpret_cast<const f32x4*>(bni + co);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = (v[r] - m[r]) * s[r];
+        }
+        const bool primary = co < p.ysplit;
+        if ((flags & EPI_RES) && primary) {
+          float rv[4];
+          load4(R + pix * p.ldr + co, rv);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] += rv[r];
+        }
+        if (flags & EPI_RELU) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+        }
+        if (primary) store4(Y + pix * p.ldy + co, v);
+        else store4(Y2 + pix * p.ldy2 + (co - p.ysplit), v);
+      } else {
+        for (int r = 0; r < 4; ++r) {
+          const int c = co + r;
+          if (c >= p.Cout) break;
+          float x = v[r];
+          if (flags & EPI_PRE_RELU) x = fmaxf(x, 0.f);
+          if (flags & EPI_AFFINE) x = (x - bnm[c]) * bni[c];
+          const bool primary = c < p.ysplit;
+          if ((flags & EPI_RES) && primary) x += (float)R[pix * p.ldr + c];
+          if (flags & EPI_RELU) x = fmaxf(x, 0.f);
+          if (primary) Y[pix * p.ldy + c] = (T)x;
+          else Y2[pix * p.ldy2 + (c - p.ysplit)] = (T)x;
+        }
+      }
+    }
+  }
+}
+
+int conv_kstep(DType t) { return t == BF16 ? Tr<bf16_t>::KSTEP : Tr<float>::KSTEP; }
+int conv_vec(DType t) { return t == BF16 ? Tr<bf16_t>::VEC : Tr<float>::VEC; }
+
+template <typename T, int WCO, int WPX>
+static hipError_t launch_t(const ConvParams& p, const ConvLaunch& l, hipStream_t s) {
+  const int M = p.N * p.Ho * p.Wo;
+  dim3 grid((M + 64 * WPX - 1) / (64 * WPX), p.groups * p.cblocks, l.splitk > 0 ? l.splitk : 1);
+  if (l.vec)
+    hipLaunchKernelGGL((conv_igemm<T, WCO, WPX, true>), grid, dim3(256), 0, s, p);
+  else
+    hipLaunchKernelGGL((conv_igemm<T, WCO, WPX, false>), grid, dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+template <typename T, int WPX>
+static hipError_t launch_wco(const ConvParams& p, const ConvLaunch& l, hipStream_t s) {
+  switch (l.wco) {
+    case 1: return launch_t<T, 1, WPX>(p, l, s);
+    case 2: return launch_t<T, 2, WPX>(p, l, s);
+    case 3: return launch_t<T, 3, WPX>(p, l, s);
+    case 4: return launch_t<T, 4, WPX>(p, l, s);
+    case 6: return launch_t<T, 6, WPX>(p, l, s);
+    case 8: return launch_t<T, 8, WPX>(p, l, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+template <typename T>
+static hipError_t launch_wpx(const ConvParams& p, const ConvLaunch& l, hipStream_t s) {
+  switch (l.wpx) {
+    case 1: return launch_wco<T, 1>(p, l, s);
+    case 2: return launch_wco<T, 2>(p, l, s);
+    case 4: return launch_wco<T, 4>(p, l, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_conv(DType t, const ConvParams& p, const ConvLaunch& l, hipStream_t s) {
+  return t == BF16 ? launch_wpx<bf16_t>(p, l, s) : launch_wpx<float>(p, l, s);
+}
+
+// ----------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void splitk_reduce(const float* __restrict__ partial, int S,
+                                                     int M, int coutp, int cout,
+                                                     const float* __restrict__ mean,
+                                                     const float* __restrict__ inv, int flags,
+                                                     float* __restrict__ out, int ldo) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)M * cout) return;
+  const int pix = (int)(idx / cout), c = (int)(idx - (int64_t)pix * cout);
+  float v = 0.f;
+  for (int z = 0; z < S; ++z) v += partial[((size_t)z * M + pix) * coutp + c];
+  if (flags & EPI_PRE_RELU) v = fmaxf(v, 0.f);
+  if (flags & EPI_AFFINE) v = (v - mean[c]) * inv[c];
+  if (flags & EPI_RELU) v = fmaxf(v, 0.f);
+  out[(size_t)pix * ldo + c] = v;
+}
+
+hipError_t launch_splitk_reduce(const float* partial, int S, int M, int coutp, int cout,
+                                const float* mean, const float* inv, int flags, float* out,
+                                int ldo, hipStream_t s) {
+  int64_t n = (int64_t)M * cout;
+  hipLaunchKernelGGL(splitk_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, partial,
+                     S, M, coutp, cout, mean, inv, flags, out, ldo);
+  return hipGetLastError();
+}
+
+// ----------------------------------------------------------------------------
+// Stats pool over H (time) of NHWC [N,H,W,C] + head BN on the pooled vector.
+// Block = (64 column-chunks) x TS time-slices.  A column chunk is VN
+// consecutive channels of one (n, w); slices sum strided rows, then the
+// slice partials are combined in fixed order through LDS (deterministic),
+// first for the mean and then for the centred second moment (two-pass, as
+// tf.nn.moments).  out[n][w*2C + c] = mean, out[n][w*2C + C + c] = std.
+template <typename T, int VN, int TS>
+__global__ __launch_bounds__(64 * TS) void stats_pool_k(const T* __restrict__ x, int N, int H,
+                                                        int W, int C,
+                                                        const float* __restrict__ mean,
+                                                        const float* __restrict__ inv,
+                                                        float* __restrict__ out) {
+  __shared__ float red[TS][64][VN];
+  __shared__ float mu_s[64][VN];
+  const int cx = threadIdx.x & 63, ts = threadIdx.x >> 6;
+  const int chunks = C / VN;
+  const int64_t gcol = (int64_t)blockIdx.x * 64 + cx;  // over N*W*chunks
+  const bool valid = gcol < (int64_t)N * W * chunks;
+  int n = 0, w = 0, ch = 0;
+  if (valid) {
+    n = (int)(gcol / ((int64_t)W * chunks));
+    int r = (int)(gcol - (int64_t)n * W * chunks);
+    w = r / chunks;
+    ch = r - w * chunks;
+  }
+  const size_t rowstride = (size_t)W * C;
+  const T* base = x + ((size_t)n * H * W + w) * C + (size_t)ch * VN;
+  float s[VN];
+#pragma unroll
+  for (int e = 0; e < VN; ++e) s[e] = 0.f;
+  if (valid) {
+    for (int h = ts; h < H; h += TS) {
+      const T* q = base + (size_t)h * rowstride;
+#pragma unroll
+      for (int e = 0; e < VN; ++e) s[e] += (float)q[e];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < VN; ++e) red[ts][cx][e] = s[e];
+  __syncthreads();
+  if (ts == 0) {
+#pragma unroll
+    for (int e = 0; e < VN; ++e) {
+      float t = 0.f;
+      for (int k = 0; k < TS; ++k) t += red[k][cx][e];
+      mu_s[cx][e] = t / (float)H;
+    }
+  }
+  __syncthreads();
+  float mu[VN];
+#pragma unroll
+  for (int e = 0; e < VN; ++e) { mu[e] = mu_s[cx][e]; s[e] = 0.f; }
+  if (valid) {
+    for (int h = ts; h < H; h += TS) {
+      const T* q = base + (size_t)h * rowstride;
+#pragma unroll
+      for (int e = 0; e < VN; ++e) {
+        float d = (float)q[e] - mu[e];
+        s[e] += d * d;
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < VN; ++e) red[ts][cx][e] = s[e];
+  __syncthreads();
+  if (ts == 0 && valid) {
+    float* o = out + (size_t)n * W * 2 * C + (size_t)w * 2 * C + (size_t)ch * VN;
+#pragma unroll
+    for (int e = 0; e < VN; ++e) {
+      float t = 0.f;
+      for (int k = 0; k < TS; ++k) t += red[k][cx][e];
+      float sd = sqrtf(t / (float)H + 1e-5f);
+      float m = mu[e];
+      const int fm = w * 2 * C + ch * VN + e, fs = fm + C;
+      if (mean) {
+        m = (m - mean[fm]) * inv[fm];
+        sd = (sd - mean[fs]) * inv[fs];
+      }
+      o[e] = m;
+      o[C + e] = sd;
+    }
+  }
+}
+
+template <typename T, int VN>
+static hipError_t stats_pool_ts(const T* x, int N, int H, int W, int C, const float* mean,
+                                const float* inv, float* out, hipStream_t s) {
+  const int64_t cols = (int64_t)N * W * (C / VN);
+  const unsigned blocks = (unsigned)((cols + 63) / 64);
+  // more time-slices when there are few columns or many frames
+  if (H >= 64 && blocks < 2048) {
+    hipLaunchKernelGGL((stats_pool_k<T, VN, 8>), dim3(blocks), dim3(64 * 8), 0, s, x, N, H, W, C,
+                       mean, inv, out);
+  } else if (H >= 16) {
+    hipLaunchKernelGGL((stats_pool_k<T, VN, 4>), dim3(blocks), dim3(64 * 4), 0, s, x, N, H, W, C,
+                       mean, inv, out);
+  } else {
+    hipLaunchKernelGGL((stats_pool_k<T, VN, 1>), dim3(blocks), dim3(64), 0, s, x, N, H, W, C,
+                       mean, inv, out);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_stats_pool(DType t, const void* x, int N, int H, int W, int C,
+                             const float* mean, const float* inv, float* out, hipStream_t s) {
+  if (t == BF16) {
+    if (C % 8 == 0)
+      return stats_pool_ts<bf16_t, 8>((const bf16_t*)x, N, H, W, C, mean, inv, out, s);
+    if (C % 2 == 0)
+      return stats_pool_ts<bf16_t, 2>((const bf16_t*)x, N, H, W, C, mean, inv, out, s);
+    return stats_pool_ts<bf16_t, 1>((const bf16_t*)x, N, H, W, C, mean, inv, out, s);
+  }
+  if (C % 4 == 0)
+    return stats_pool_ts<float, 4>((const float*)x, N, H, W, C, mean, inv, out, s);
+  return stats_pool_ts<float, 1>((const float*)x, N, H, W, C, mean, inv, out, s);
+}
+
+// ----------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void avgpool3s2_k(const T* __restrict__ x, int ldx, int N,
+                                                    int H, int W, int C, T* __restrict__ y,
+                                                    int ldy, int Ho, int Wo) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)N * Ho * Wo * C) return;
+  const int c = (int)(idx % C);
+  const int64_t pix = idx / C;
+  const int wo = (int)(pix % Wo);
+  const int ho = (int)((pix / Wo) % Ho);
+  const int n = (int)(pix / ((int64_t)Wo * Ho));
+  float s = 0.f;
+  for (int ky = 0; ky < 3; ++ky) {
+    const int hi = 2 * ho - 1 + ky;
+    if (hi < 0 || hi >= H) continue;
+    for (int kx = 0; kx < 3; ++kx) {
+      const int wi = 2 * wo - 1 + kx;
+      if (wi < 0 || wi >= W) continue;
+      s += (float)x[(((size_t)n * H + hi) * W + wi) * ldx + c];
+    }
+  }
+  y[pix * ldy + c] = (T)(s / 9.0f);
+}
+
+hipError_t launch_avgpool3s2(DType t, const void* x, int ldx, int N, int H, int W, int C,
+                             void* y, int ldy, int Ho, int Wo, hipStream_t s) {
+  const int64_t n = (int64_t)N * Ho * Wo * C;
+  const unsigned g = (unsigned)((n + 255) / 256);
+  if (t == BF16)
+    hipLaunchKernelGGL(avgpool3s2_k<bf16_t>, dim3(g), dim3(256), 0, s, (const bf16_t*)x, ldx, N,
+                       H, W, C, (bf16_t*)y, ldy, Ho, Wo);
+  else
+    hipLaunchKernelGGL(avgpool3s2_k<float>, dim3(g), dim3(256), 0, s, (const float*)x, ldx, N, H,
+                       W, C, (float*)y, ldy, Ho, Wo);
+  return hipGetLastError();
+}
+
+// ----------------------------------------------------------------------------
+__global__ void convert_f32_bf16(const float* __restrict__ x, bf16_t* __restrict__ y, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) y[i] = (bf16_t)x[i];
+}
+
+hipError_t launch_convert_f32(DType t, const float* x, void* y, int64_t n, hipStream_t s) {
+  if (t == F32) return hipMemcpyAsync(y, x, n * 4, hipMemcpyDeviceToDevice, s);
+  hipLaunchKernelGGL(convert_f32_bf16, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x,
+                     (bf16_t*)y, n);
+  return hipGetLastError();
+}
+
+template <typename T>
+__global__ void copy_channels_k(const T* __restrict__ x, int ldx, T* __restrict__ y, int ldy,
+                                int64_t npix, int C) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= npix * C) return;
+  const int64_t p = i / C;
+  const int c = (int)(i - p * C);
+  y[p * ldy + c] = x[p * ldx + c];
+}
+
+hipError_t launch_copy_channels(DType t, const void* x, int ldx, void* y, int ldy, int64_t npix,
+                                int C, hipStream_t s) {
+  const int64_t n = npix * C;
+  const unsigned g = (unsigned)((n + 255) / 256);
+  if (t == BF16)
+    hipLaunchKernelGGL(copy_channels_k<bf16_t>, dim3(g), dim3(256), 0, s, (const bf16_t*)x, ldx,
+                       (bf16_t*)y, ldy, npix, C);
+  else
+    hipLaunchKernelGGL(copy_channels_k<float>, dim3(g), dim3(256), 0, s, (const float*)x, ldx,
+                       (float*)y, ldy, npix, C);
+  return hipGetLastError();
+}
+
+// In-place BN+ReLU over a channel prefix [npix][C] of a buffer with stride ld
+// (DPN concat_bn_relu, dpn_model.py:24-29).
+template <typename T>
+__global__ void bnrelu_k(T* __restrict__ x, int ld, int64_t npix, int C,
+                         const float* __restrict__ mean, const float* __restrict__ inv) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= npix * C) return;
+  const int64_t p = i / C;
+  const int c = (int)(i - p * C);
+  T* q = x + p * ld + c;
+  *q = (T)fmaxf(((float)*q - mean[c]) * inv[c], 0.f);
+}
+
+hipError_t launch_bnrelu_inplace(DType t, void* x, int ld, int64_t npix, int C, const float* mean,
+                                 const float* inv, hipStream_t s) {
+  const int64_t n = npix * C;
+  const unsigned g = (unsigned)((n + 255) / 256);
+  if (t == BF16)
+    hipLaunchKernelGGL(bnrelu_k<bf16_t>, dim3(g), dim3(256), 0, s, (bf16_t*)x, ld, npix, C, mean,
+                       inv);
+  else
+    hipLaunchKernelGGL(bnrelu_k<float>, dim3(g), dim3(256), 0, s, (float*)x, ld, npix, C, mean,
+                       inv);
+  return hipGetLastError();
+}
+
+}  // namespace vox

@@ -1,0 +1,128 @@
+"""Python mirror of the reference's model-session interface.
+
+The reference (tensorflow/tf_extract.py:75-111) imports a frozen graph and
+calls `sess.run(outputs, {inputs: x})` once per <=1000-frame chunk of each
+utterance.  `Extractor` is that session: it loads a weight blob into
+libvoxemb on one HIP device and exposes
+
+  * `run(x)`        -- one batch [N,T,F] (host numpy) -> [N,D]   (sess.run)
+  * `run_device(...)` -- device-resident in/out (torch tensors)
+  * `embed_utterance(feat)` -- the chunk rule + length-weighted average
+                               (tf_extract.py:96-111), with the reference's
+                               failure for T < 25 (ZeroDivisionError).
+
+All compute is in the HIP library; there is no CPU fallback.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import _native
+from ._native import check, fptr, lib
+
+MAX_FRAMES = 1000  # tf_extract.py:96
+MIN_FRAMES = 25    # tf_extract.py:101-102
+
+
+def chunk_plan(T, max_frames=MAX_FRAMES):
+    """[(start, length)] per tf_extract.py:102-107 (empty for T < 25)."""
+    n = 1 + (T - 25) // max_frames
+    out = []
+    for i in range(max(n, 0)):
+        L = max_frames if (i + 1) * max_frames <= T else T - i * max_frames
+        out.append((i * max_frames, L))
+    return out
+
+
+class Extractor:
+    def __init__(self, weights, device=0, precision="bf16"):
+        prec = {"fp32": _native.VOX_FP32, "bf16": _native.VOX_BF16}[precision]
+        h = C.c_void_p()
+        L = lib()
+        if isinstance(weights, (bytes, bytearray)):
+            buf = C.create_string_buffer(bytes(weights), len(weights))
+            check(L.vox_load_blob(buf, len(weights), int(device), prec, C.byref(h)))
+        else:
+            check(L.vox_load(os.fsencode(weights), int(device), prec, C.byref(h)))
+        self._h = h
+        self.device = int(device)
+        self.precision = precision
+        self.dim = check(L.vox_dim(h))
+        self.feat_dim = check(L.vox_feat_dim(h))
+        self.expand_dim = check(L.vox_expand_dim(h))
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().vox_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # -- sess.run ---------------------------------------------------------
+    def run(self, x):
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        if x.ndim != 3:
+            raise ValueError("expected [N, T, F] features")
+        n, t, f = x.shape
+        out = np.empty((n, self.dim), np.float32)
+        check(lib().vox_embed(self._h, fptr(x), n, t, f, fptr(out)))
+        return out
+
+    def run_device(self, x, out=None, stream=None):
+        """x: contiguous float32 torch tensor [N,T,F] on this device.  Returns
+        (or fills) a float32 [N,D] device tensor.  Launches on `stream`
+        (torch.cuda.Stream or raw handle) -- the current torch stream by default."""
+        import torch
+        if x.dtype != torch.float32 or not x.is_contiguous() or x.dim() != 3:
+            raise ValueError("expected a contiguous float32 [N,T,F] device tensor")
+        n, t, f = x.shape
+        if out is None:
+            out = torch.empty((n, self.dim), dtype=torch.float32, device=x.device)
+        if stream is None:
+            stream = torch.cuda.current_stream(x.device)
+        sh = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
+        check(lib().vox_embed_device(self._h, C.c_void_p(x.data_ptr()), n, t, f,
+                                     C.c_void_p(out.data_ptr()), C.c_void_p(sh)))
+        return out
+
+    def profile(self, x, reps=5, stream=None, max_ops=4096):
+        """Per-op timing of one forward (HIP events around each launch)."""
+        import torch
+        n, t, f = x.shape
+        ms = np.zeros(max_ops, np.float32)
+        fl = np.zeros(max_ops, np.float64)
+        by = np.zeros(max_ops, np.float64)
+        kind = np.zeros(max_ops, np.int32)
+        if stream is None:
+            stream = torch.cuda.current_stream(x.device)
+        sh = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
+        nops = check(lib().vox_profile(
+            self._h, C.c_void_p(x.data_ptr()), n, t, f, int(reps), fptr(ms),
+            fl.ctypes.data_as(C.POINTER(C.c_double)), by.ctypes.data_as(C.POINTER(C.c_double)),
+            kind.ctypes.data_as(C.POINTER(C.c_int)), max_ops, C.c_void_p(sh)))
+        return dict(ms=ms[:nops], flops=fl[:nops], bytes=by[:nops], kind=kind[:nops])
+
+    # -- tf_extract chunk loop ---------------------------------------------
+    def embed_utterance(self, feat):
+        feat = np.ascontiguousarray(feat, dtype=np.float32)
+        T, f = feat.shape
+        if T < MIN_FRAMES:
+            # the reference divides 0 by 0 here (tf_extract.py:111)
+            raise ZeroDivisionError(f"utterance has {T} < {MIN_FRAMES} frames")
+        out = np.empty(self.dim, np.float32)
+        check(lib().vox_embed_utt(self._h, fptr(feat), T, f, fptr(out)))
+        return out
