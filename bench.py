@@ -32,6 +32,12 @@ PEAK_HBM_GBS = 8000.0       # HBM3E spec
 
 def _kernel_name(tag, dt):
     kind = tag & 15
+    if tag & (1 << 21):
+        return "gemm1x1_lds"
+    if tag & (1 << 20):
+        return f"conv1x1_rr<{(tag >> 16) & 15}, {(tag >> 8) & 15}, {(tag >> 4) & 15}>"
+    if tag & (1 << 15):
+        return f"conv_win<{(tag >> 4) & 15}, {(tag >> 8) & 15}>"
     if tag & (1 << 14):
         wco, wpx, vec = (tag >> 4) & 15, (tag >> 8) & 15, (tag >> 12) & 1
         t = "float" if tag & (1 << 13) else "__bf16"
@@ -97,6 +103,7 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dump-ops", action="store_true", help="print per-op timing to stderr")
     ap.add_argument("--cache-dir", default=os.environ.get("VOXEMB_CACHE", "/tmp/voxemb_cache"))
     args = ap.parse_args()
 
@@ -152,6 +159,10 @@ def main():
 
     # ---- per-kernel timing (HIP events around every launch, same stream)
     prof = ex.profile(x, reps=5, stream=stream)
+    if args.dump_ops and rank == 0:
+        desc = ex.describe(x)
+        for d, ms in zip(desc, prof["ms"]):
+            print(f"{ms*1e3:9.1f} us  {d}", file=sys.stderr)
     groups = {}
     for ms, fl, by, tag in zip(prof["ms"], prof["flops"], prof["bytes"], prof["kind"]):
         g = groups.setdefault(_kernel_name(int(tag), args.precision),
@@ -160,7 +171,7 @@ def main():
         g["flops"] += float(fl)
         g["bytes"] += float(by)
         g["n"] += 1
-    conv = {k: v for k, v in groups.items() if k.startswith("conv_igemm")}
+    conv = {k: v for k, v in groups.items() if k.startswith("conv_")}
     dom_name, dom = max(conv.items(), key=lambda kv: kv[1]["ms"])
     peak = PEAK_F32_TFLOPS if "float" in dom_name else PEAK_BF16_TFLOPS
     ach = (dom["flops"] / dom["n"]) / (dom["ms"] / dom["n"] * 1e-3) / 1e12

@@ -84,6 +84,12 @@ int vox_profile(vox_model* m, const float* d_x, int n, int t, int f, int reps,
                 float* op_ms, double* op_flops, double* op_bytes, int* op_kind,
                 int max_ops, void* stream);
 
+/* Text description of the plan at (n, t): one line per kernel launch with
+ * its kernel family, tile config, shapes and algorithmic FLOP/bytes.
+ * Returns the needed buffer size (bytes incl. NUL) or a status (<0). */
+int vox_plan_describe(vox_model* m, const float* d_x, int n, int t, int f, char* buf,
+                      size_t cap);
+
 /* Standalone stats-pool (+BN) kernel: x NHWC [n,h,w,c] (dtype VOX_FP32 or
  * VOX_BF16), mean/inv per pooled feature (may be NULL = identity),
  * out [n, w*2c] float32 with feature index w*2c + {c | c+C}. */

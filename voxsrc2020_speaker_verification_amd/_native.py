@@ -40,6 +40,8 @@ _SIGS = [
     ("vox_profile", C.c_int, [_P, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, _F,
                               C.POINTER(C.c_double), C.POINTER(C.c_double),
                               C.POINTER(C.c_int), C.c_int, _P]),
+    ("vox_plan_describe", C.c_int, [_P, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_char_p,
+                                    C.c_size_t]),
     ("vox_stats_pool_device", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
                                         C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, _P]),
     ("vox_last_error", C.c_char_p, []),

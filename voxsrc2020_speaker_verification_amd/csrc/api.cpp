@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <map>
@@ -153,6 +154,8 @@ struct ConvW {
   int kh = 1, kw = 1, cin = 0, cout = 0, groups = 1;  // cin/cout per group
   int coutp = 0, cinp = 0, kp = 0, wco = 1, vec = 1;
   std::shared_ptr<DevBuf> w;         // [groups][coutp][kp] in the model dtype
+  std::shared_ptr<DevBuf> wtc;       // bf16 [coutp][taps*cin] for conv_win (groups == 1)
+  std::shared_ptr<DevBuf> wpair;     // bf16 [coutp][kp] paired-row layout for conv1x1_rr
   std::shared_ptr<DevBuf> mean, inv; // optional epilogue BN (cout*groups)
 };
 
@@ -207,6 +210,10 @@ struct vox_model {
   float* plan_out = nullptr;
   std::vector<Op> plan;
   DevBuf stage_in, stage_out;  // host-API staging
+  bool no_win = false;         // VOXEMB_NO_WIN=1: disable conv_win (A/B testing)
+  bool no_rr = false;          // VOXEMB_NO_RR=1: disable conv1x1_rr
+  bool no_gemm = false;        // VOXEMB_NO_GEMM=1: disable gemm1x1_lds
+  int rr_wpx = 0, rr_wco = 0;  // VOXEMB_RR_WPX / VOXEMB_RR_WCO: tile overrides (tuning)
 };
 
 static size_t esize(DType t) { return t == BF16 ? 2 : 4; }
@@ -253,6 +260,33 @@ static int make_conv(vox_model* m, const HostTensor& k, int groups, const HostTe
     HIPCHK(hipMemcpy(out.w->p, h.data(), h.size() * 2, hipMemcpyHostToDevice));
   } else {
     HIPCHK(hipMemcpy(out.w->p, w.data(), w.size() * 4, hipMemcpyHostToDevice));
+  }
+  if (dt == BF16 && groups == 1 && taps == 1 && out.vec && out.coutp % 32 == 0) {
+    // paired rows: row (2q+u)*16 + 4g + e <- channel 32q + 8g + 4u + e
+    std::vector<uint16_t> h((size_t)out.coutp * out.kp, 0);
+    for (int row = 0; row < out.coutp; ++row) {
+      const int q = row / 32, u = (row / 16) & 1, g = (row & 15) / 4, e = row & 3;
+      const int co = 32 * q + 8 * g + 4 * u + e;
+      if (co >= cout) continue;
+      for (int ci = 0; ci < cin; ++ci)
+        h[(size_t)row * out.kp + ci] = f2bf(k.data[(size_t)ci * cout_all + col0 + co]);
+    }
+    out.wpair = std::make_shared<DevBuf>();
+    HIPCHK(out.wpair->ensure(h.size() * 2));
+    HIPCHK(hipMemcpy(out.wpair->p, h.data(), h.size() * 2, hipMemcpyHostToDevice));
+  }
+  if (dt == BF16 && groups == 1 && cin % 8 == 0) {
+    std::vector<uint16_t> h((size_t)out.coutp * taps * cin, 0);
+    for (int co = 0; co < cout; ++co)
+      for (int t = 0; t < taps; ++t)
+        for (int ci = 0; ci < cin; ++ci) {
+          const int ky = t / kw, kx = t % kw;
+          h[((size_t)co * taps + t) * cin + ci] =
+              f2bf(k.data[(((size_t)ky * kw + kx) * cin + ci) * cout_all + col0 + co]);
+        }
+    out.wtc = std::make_shared<DevBuf>();
+    HIPCHK(out.wtc->ensure(h.size() * 2));
+    HIPCHK(hipMemcpy(out.wtc->p, h.data(), h.size() * 2, hipMemcpyHostToDevice));
   }
   if (bm) {
     const int C = (int)bm->data.size();
@@ -441,6 +475,66 @@ static void emit_conv(Builder& B, const ConvW& cw, Act x, const void* x2, int ld
   op.cl.splitk = 1;
   const int M = x.N * Ho * Wo;
   op.cl.wpx = M >= 64 * 4 * 512 ? 4 : (M >= 64 * 2 * 256 ? 2 : 1);
+  // bf16 1x1 with K <= 256: register-resident activations, all couts per wave
+  const int ks_rr = (cw.cinp + 31) / 32;
+  if (B.m->dt == BF16 && dt_override != F32 && cw.wpair && !(flags & EPI_PARTIAL) &&
+      !B.m->no_rr && ph == 0 && pw == 0 && cw.cout % 8 == 0 && ldy % 8 == 0 &&
+      (ysplit >= (1 << 30) || (ysplit % 8 == 0 && ldy2 % 8 == 0)) && (!res || ldr % 8 == 0) &&
+      x.ld % 8 == 0 &&
+      (ks_rr == 1 || ks_rr == 2 || ks_rr == 3 || ks_rr == 4 || ks_rr == 6 || ks_rr == 8 ||
+       ks_rr == 12 || ks_rr == 16 || ks_rr == 24 || ks_rr == 32)) {
+    op.type = 8;
+    p.w = cw.wpair->p;
+    op.cl.wco = 2;  // measured best (tools/sweep_rr.sh): occupancy over tile size
+    // enough waves: pixel tiles x cout ranges >= ~2048 blocks' worth
+    int wpx = conv1x1_rr_max_wpx(ks_rr);
+    while (wpx > 1 && (M + 64 * wpx - 1) / (64 * wpx) < 1024) wpx /= 2;
+    if (B.m->rr_wpx > 0) wpx = std::min(wpx, B.m->rr_wpx);
+    if (B.m->rr_wco > 0 && (cw.coutp / 16) % B.m->rr_wco == 0) op.cl.wco = B.m->rr_wco;
+    op.cl.wpx = wpx;
+    const int gx = (M + 64 * wpx - 1) / (64 * wpx);
+    const int tiles = cw.coutp / 16;
+    int ys = 1;
+    while (gx * ys < 1024 && tiles / (ys * 2) >= op.cl.wco) ys *= 2;
+    op.cl.splitk = ys;
+    // compute-bound shapes: LDS-tiled 128x128 GEMM
+    if (!B.m->no_gemm && !in_mean && cw.cinp % 64 == 0 && cw.cinp >= 256 && cw.coutp % 128 == 0 &&
+        cw.cout >= 256)
+      op.type = 9;
+  }
+  // stride-1 bf16 convs without prologue: window-staged LDS kernel if it fits
+  if (op.type == 0 && B.m->dt == BF16 && dt_override != F32 && cw.wtc && sh == 1 && sw == 1 && !in_mean &&
+      Ho == x.H && Wo == x.W && !(flags & EPI_PARTIAL) && !B.m->no_win) {
+    const int taps = cw.kh * cw.kw;
+    const int minoff = -(ph * x.W + pw);
+    const int maxoff = ((cw.kh - 1) * dh - ph) * x.W + (cw.kw - 1) * dw - pw;
+    const int BCO = 16 * cw.wco;
+    const int kcs[] = {cw.cin, 256, 128, 64, 32};
+    bool done = false;
+    for (int wpx : {4, 2, 1}) {
+      if (done) break;
+      if (wpx > 1 && M < 64 * wpx * 256) continue;  // keep >= 256 blocks when possible
+      for (int kc : kcs) {
+        if (kc > cw.cin || kc % 8) continue;
+        if (kc != cw.cin && kc > 128) continue;
+        int au = kc / 8;
+        if (!(au & 1)) ++au;
+        const int kcp = (taps * kc + 31) / 32 * 32;
+        int wu = kcp / 8;
+        if (!(wu & 1)) ++wu;
+        const int len = 64 * wpx + maxoff - minoff;
+        const int lds = len * au * 16 + BCO * wu * 16 + (kcp / 8) * 16;
+        if (lds > 64 * 1024) continue;
+        p.win_lo = minoff; p.win_len = len; p.win_kc = kc;
+        p.win_astr = au * 16; p.win_wstr = wu * 16; p.win_lds = lds;
+        p.w = cw.wtc->p;
+        op.cl.wpx = wpx;
+        op.type = 7;
+        done = true;
+        break;
+      }
+    }
+  }
   const double es = dt_override == F32 ? 4.0 : (double)es_of(B.m);
   op.flops = 2.0 * M * cw.cout * cw.groups * (double)cw.kh * cw.kw * cw.cin;
   op.bytes = es * ((double)x.N * x.H * x.W * cw.cin * cw.groups * (x2 ? 2 : 1) +
@@ -728,6 +822,9 @@ static int build_plan(vox_model* m, const float* x, int n, int t, float* out) {
 static hipError_t run_op(vox_model* m, const Op& op, hipStream_t s) {
   switch (op.type) {
     case 0: return launch_conv(m->dt, op.cp, op.cl, s);
+    case 7: return launch_conv_win(op.cp, op.cl, s);
+    case 8: return launch_conv1x1_rr(op.cp, op.cl, s);
+    case 9: return launch_gemm1x1(op.cp, s);
     case 5: return launch_conv(F32, op.cp, op.cl, s);
     case 1:
       return launch_splitk_reduce(op.part, op.S, op.M, op.coutp, op.cout, op.mean, op.inv,
@@ -777,6 +874,11 @@ extern "C" int vox_load_blob(const void* blob, size_t nbytes, int device, int pr
   m->family = spec.get("family");
   m->feat_dim = spec.geti("feat_dim");
   m->expand_dim = spec.geti("expand_dim", 3);
+  if (const char* e = std::getenv("VOXEMB_NO_WIN")) m->no_win = std::atoi(e) != 0;
+  if (const char* e = std::getenv("VOXEMB_NO_RR")) m->no_rr = std::atoi(e) != 0;
+  if (const char* e = std::getenv("VOXEMB_RR_WPX")) m->rr_wpx = std::atoi(e);
+  if (const char* e = std::getenv("VOXEMB_NO_GEMM")) m->no_gemm = std::atoi(e) != 0;
+  if (const char* e = std::getenv("VOXEMB_RR_WCO")) m->rr_wco = std::atoi(e);
   if ((rc = load_weights(m.get(), ts))) return rc;
   HIPCHK(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking));
   *out = m.release();
@@ -894,13 +996,52 @@ extern "C" int vox_profile(vox_model* m, const float* d_x, int n, int t, int f, 
       // launches by template instantiation, as rocprof names them
       const Op& o = m->plan[i];
       int tag = o.kind;
-      if (o.type == 0 || o.type == 5)
+      if (o.type == 7)
+        tag |= (o.cl.wco << 4) | (o.cl.wpx << 8) | (1 << 15);
+      else if (o.type == 9)
+        tag |= (1 << 21);
+      else if (o.type == 8)
+        tag |= (o.cl.wco << 4) | (o.cl.wpx << 8) | (((o.cp.cinp + 31) / 32) << 16) | (1 << 20);
+      else if (o.type == 0 || o.type == 5)
         tag |= (o.cl.wco << 4) | (o.cl.wpx << 8) | (o.cl.vec << 12) |
                ((o.type == 5 || m->dt == F32) ? 1 << 13 : 0) | (1 << 14);
       op_kind[i] = tag;
     }
   }
   return nops;
+}
+
+extern "C" int vox_plan_describe(vox_model* m, const float* d_x, int n, int t, int f, char* buf,
+                                 size_t cap) {
+  if (!m || !d_x) return fail(VOX_EINVAL, "null argument");
+  int rc = check_shape(m, n, t, f);
+  if (rc) return rc;
+  HIPCHK(hipSetDevice(m->device));
+  HIPCHK(m->stage_out.ensure((size_t)n * m->out_dim * 4));
+  if ((rc = ensure_plan(m, d_x, n, t, (float*)m->stage_out.p))) return rc;
+  std::string out;
+  static const char* tn[] = {"igemm", "reduce", "pool", "avgpool", "convert", "igemm32", "bnrelu",
+                             "win", "rr", "gemm"};
+  for (const Op& o : m->plan) {
+    char line[256];
+    const ConvParams& p = o.cp;
+    if (o.type == 0 || o.type == 5 || o.type == 7 || o.type == 8 || o.type == 9)
+      std::snprintf(line, sizeof(line),
+                    "%s wco=%d wpx=%d s=%d N=%d H=%d W=%d Cin=%d Ho=%d Wo=%d Cout=%d k=%dx%d st=%d "
+                    "g=%d flags=%d x2=%d pro=%d flops=%.4g bytes=%.4g\n",
+                    tn[o.type], o.cl.wco, o.cl.wpx, o.cl.splitk, p.N, p.H, p.W, p.Cin, p.Ho, p.Wo,
+                    p.Cout, p.kh, p.kw, p.sh, p.groups, p.flags, p.x2 ? 1 : 0, p.in_mean ? 1 : 0,
+                    o.flops, o.bytes);
+    else
+      std::snprintf(line, sizeof(line), "%s N=%d H=%d W=%d C=%d bytes=%.4g\n", tn[o.type], o.N,
+                    o.H, o.W, o.C, o.bytes);
+    out += line;
+  }
+  if (buf && cap > 0) {
+    std::strncpy(buf, out.c_str(), cap - 1);
+    buf[cap - 1] = 0;
+  }
+  return (int)out.size() + 1;
 }
 
 extern "C" int vox_stats_pool_device(const void* d_x, int dtype, int n, int h, int w, int c,

@@ -34,6 +34,8 @@ struct ConvParams {
   int fast4;                               // 4-channel vector epilogue allowed
   int groups;                              // grouped conv (Cin/Cout are per group)
   int cblocks;                             // cout blocks per group (gridDim.y = groups*cblocks)
+  // window-staged kernel (conv_win) geometry, see launch_conv_win
+  int win_lo, win_len, win_kc, win_astr, win_wstr, win_lds;
 };
 
 struct ConvLaunch {
@@ -44,6 +46,18 @@ struct ConvLaunch {
 
 // Returns hipSuccess or the launch error.
 hipError_t launch_conv(DType t, const ConvParams& p, const ConvLaunch& l, hipStream_t s);
+// Stride-1 bf16 conv with the input window staged in LDS (weights in the
+// [coutp][taps*Cin] layout).
+hipError_t launch_conv_win(const ConvParams& p, const ConvLaunch& l, hipStream_t s);
+// bf16 1x1 conv (any stride), cinp/32 in {1,2,3,4,6,8,12,16,24,32}:
+// activations register-resident, all cout tiles swept per wave.  Weights in
+// the paired-row layout (see kernels.hip), Cout % 8 == 0, ysplit % 8 == 0.
+// l.wco in {2,4}; l.wpx <= conv1x1_rr_max_wpx(ks); l.splitk = cout ranges.
+hipError_t launch_conv1x1_rr(const ConvParams& p, const ConvLaunch& l, hipStream_t s);
+int conv1x1_rr_max_wpx(int ks);
+// bf16 1x1 conv as an LDS-tiled GEMM (128x128 tile, BK 64): cinp % 64 == 0,
+// coutp % 128 == 0, paired-row weights, Cout/ysplit/ld multiples of 8.
+hipError_t launch_gemm1x1(const ConvParams& p, hipStream_t s);
 int conv_kstep(DType t);   // 32 (bf16) / 16 (fp32)
 int conv_vec(DType t);     // elements per 16-byte lane load: 8 / 4
 

@@ -96,6 +96,77 @@ __device__ __forceinline__ void load4(const float* p, float* v) {
   v[0] = r[0]; v[1] = r[1]; v[2] = r[2]; v[3] = r[3];
 }
 
+// Shared epilogue: lane holds couts co0+16i+4*(lane>>4)+r (r<4) of pixel
+// pbase+16j+(lane&15).  Applies EPI_* flags, writes y / y2 / split-K slab.
+template <typename T, int WCO, int WPX>
+__device__ __forceinline__ void conv_epilogue(const ConvParams& p, f32x4 (&acc)[WCO][WPX],
+                                              const bool (&pv)[WPX], int pbase, int co0, int grp,
+                                              int M) {
+  const int lane = threadIdx.x & 63;
+  const int col = lane & 15;
+  const int goff = grp * p.Cout;
+  T* __restrict__ Y = reinterpret_cast<T*>(p.y) + goff;
+  T* __restrict__ Y2 = reinterpret_cast<T*>(p.y2);
+  const T* __restrict__ R = p.res ? reinterpret_cast<const T*>(p.res) + goff : nullptr;
+  const float* __restrict__ bnm = p.mean ? p.mean + goff : nullptr;
+  const float* __restrict__ bni = p.inv ? p.inv + goff : nullptr;
+  const int flags = p.flags;
+#pragma unroll
+  for (int i = 0; i < WCO; ++i) {
+    const int co = co0 + 16 * i + 4 * (lane >> 4);
+    if (co >= p.Cout) continue;
+#pragma unroll
+    for (int j = 0; j < WPX; ++j) {
+      if (!pv[j]) continue;
+      const size_t pix = (size_t)(pbase + 16 * j + col);
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if (flags & EPI_PARTIAL) {
+        float* dst = p.partial + ((size_t)blockIdx.z * M + pix) * p.coutp + co;
+        *reinterpret_cast<f32x4*>(dst) = f32x4{v[0], v[1], v[2], v[3]};
+        continue;
+      }
+      if (p.fast4 && co + 3 < p.Cout) {
+        if (flags & EPI_PRE_RELU) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+        }
+        if (flags & EPI_AFFINE) {
+          f32x4 m = *reinterpret_cast<const f32x4*>(bnm + co);
+          f32x4 s = *reinterpret_cast<const f32x4*>(bni + co);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = (v[r] - m[r]) * s[r];
+        }
+        const bool primary = co < p.ysplit;
+        if ((flags & EPI_RES) && primary) {
+          float rv[4];
+          load4(R + pix * p.ldr + co, rv);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] += rv[r];
+        }
+        if (flags & EPI_RELU) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+        }
+        if (primary) store4(Y + pix * p.ldy + co, v);
+        else store4(Y2 + pix * p.ldy2 + (co - p.ysplit), v);
+      } else {
+        for (int r = 0; r < 4; ++r) {
+          const int c = co + r;
+          if (c >= p.Cout) break;
+          float x = v[r];
+          if (flags & EPI_PRE_RELU) x = fmaxf(x, 0.f);
+          if (flags & EPI_AFFINE) x = (x - bnm[c]) * bni[c];
+          const bool primary = c < p.ysplit;
+          if ((flags & EPI_RES) && primary) x += (float)R[pix * p.ldr + c];
+          if (flags & EPI_RELU) x = fmaxf(x, 0.f);
+          if (primary) Y[pix * p.ldy + c] = (T)x;
+          else Y2[pix * p.ldy2 + (c - p.ysplit)] = (T)x;
+        }
+      }
+    }
+  }
+}
+
 // ----------------------------------------------------------------------------
 // Implicit-GEMM conv.  MFMA rows = output channels (A = weights [coutp][kp]),
 // MFMA columns = output pixels (B = im2col, gathered straight from NHWC).
@@ -234,68 +305,532 @@ __global__ __launch_bounds__(256) void conv_igemm(ConvParams p) {
     }
   }
 
-  // ---------------------------------------------------------------- epilogue
-  const int goff = grp * p.Cout;
-  T* __restrict__ Y = reinterpret_cast<T*>(p.y) + goff;
-  T* __restrict__ Y2 = reinterpret_cast<T*>(p.y2);
-  const T* __restrict__ R = p.res ? reinterpret_cast<const T*>(p.res) + goff : nullptr;
-  const float* __restrict__ bnm = p.mean ? p.mean + goff : nullptr;
-  const float* __restrict__ bni = p.inv ? p.inv + goff : nullptr;
-  const int flags = p.flags;
+  conv_epilogue<T, WCO, WPX>(p, acc, pv, pbase, co0, grp, M);
+}
+
+// ----------------------------------------------------------------------------
+// Window-staged implicit GEMM for stride-1 convolutions (bf16).  A block owns
+// BP = 64*WPX consecutive output pixels and BCO = 16*WCO output channels.
+// For each chunk of kc input channels it stages into LDS
+//   * the input window: flattened pixels [p0 + lo, p0 + BP + hi) x kc channels
+//     (every tap of every output pixel is a constant flattened offset
+//     dy*W + dx away in this window; out-of-image taps are masked), with the
+//     optional hierarchical addend x2 added on the way in;
+//   * the weights of the chunk for all taps, rows [tap][kc] flattened;
+//   * a k-step table q -> (window offset, channel byte offset, dy, dx).
+// Each input pixel is read from HBM once per block instead of once per tap.
+// LDS pixel / weight-row strides are padded to an odd number of 16-B units so
+// the 16 lanes of a ds_read_b128 group hit distinct banks.
+template <int WCO, int WPX>
+__global__ __launch_bounds__(256) void conv_win(ConvParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int BCO = 16 * WCO;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int col = lane & 15;
+  const int M = p.N * p.H * p.W;
+  const int p0 = blockIdx.x * (64 * WPX);
+  const int co0 = blockIdx.y * BCO;
+  const int taps = p.kh * p.kw;
+  const int HW = p.H * p.W;
+  char* act = smem;
+  char* wts = smem + p.win_len * p.win_astr;
+  int4* ktab = reinterpret_cast<int4*>(wts + BCO * p.win_wstr);
+  const bf16_t* __restrict__ X = reinterpret_cast<const bf16_t*>(p.x);
+  const bf16_t* __restrict__ X2 = reinterpret_cast<const bf16_t*>(p.x2);
+  const bf16_t* __restrict__ Wt = reinterpret_cast<const bf16_t*>(p.w);
+  const int pbase = p0 + wave * 16 * WPX;
+
+  int hh[WPX], ww[WPX], li[WPX];
+  bool pv[WPX];
 #pragma unroll
-  for (int i = 0; i < WCO; ++i) {
-    const int co = co0 + 16 * i + 4 * (lane >> 4);
-    if (co >= p.Cout) continue;
+  for (int j = 0; j < WPX; ++j) {
+    const int pix = pbase + 16 * j + col;
+    pv[j] = pix < M;
+    const int q = pv[j] ? pix : 0;
+    const int r = q % HW;
+    hh[j] = r / p.W;
+    ww[j] = r - hh[j] * p.W;
+    li[j] = pix - p0 - p.win_lo;
+  }
+  f32x4 acc[WCO][WPX];
 #pragma unroll
-    for (int j = 0; j < WPX; ++j) {
-      if (!pv[j]) continue;
-      const size_t pix = (size_t)(pbase + 16 * j + col);
-      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      if (flags & EPI_PARTIAL) {
-        float* dst = p.partial + ((size_t)blockIdx.z * M + pix) * p.coutp + co;
-        *reinterpret_cast<f32x4*>(dst) = f32x4{v[0], v[1], v[2], v[3]};
-        continue;
+  for (int i = 0; i < WCO; ++i)
+#pragma unroll
+    for (int j = 0; j < WPX; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int c0 = 0; c0 < p.Cin; c0 += p.win_kc) {
+    const int kc = min(p.win_kc, p.Cin - c0);
+    const int kflat = taps * kc;
+    const int kcp = (kflat + 31) & ~31;
+    const int units = kcp >> 3;
+    // k-step table
+    for (int q = tid; q < units; q += 256) {
+      const int k = q * 8;
+      int4 e = make_int4(0, 0, 1 << 20, 1 << 20);
+      if (k < kflat) {
+        const int tap = k / kc, ch = k - (k / kc) * kc;
+        const int ky = tap / p.kw, kx = tap - (tap / p.kw) * p.kw;
+        const int dy = ky * p.dh - p.ph, dx = kx * p.dw - p.pw;
+        e = make_int4(dy * p.W + dx, ch * 2, dy, dx);
       }
-      if (p.fast4 && co + 3 < p.Cout) {
-        if (flags & EPI_PRE_RELU) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+      ktab[q] = e;
+    }
+    // weights [BCO][taps*kc] (global layout [coutp][taps*Cin])
+    {
+      const int total = BCO * units;
+      const int rowlen = taps * p.Cin;
+      for (int idx = tid; idx < total; idx += 256) {
+        const int r = idx / units, u = idx - (idx / units) * units;
+        const int k = u * 8;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (k < kflat) {
+          const int tap = k / kc, ch = k - (k / kc) * kc;
+          v = *reinterpret_cast<const uint4*>(Wt + (size_t)(co0 + r) * rowlen + tap * p.Cin + c0 + ch);
         }
-        if (flags & EPI_AFFINE) {
-          f32x4 m = *reinterpret_cast<const f32x4*>(bnm + co);
-          f32x4 s = *reinterpret_cast<const f32x4*>(bni + co);
+        *reinterpret_cast<uint4*>(wts + r * p.win_wstr + u * 16) = v;
+      }
+    }
+    // input window (+ addend)
+    {
+      const int cu = kc >> 3;
+      const int total = p.win_len * cu;
+      const int gbase = p0 + p.win_lo;
+      for (int b0 = tid; b0 < total; b0 += 4 * 256) {
+        uint4 v[4];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = (v[r] - m[r]) * s[r];
-        }
-        const bool primary = co < p.ysplit;
-        if ((flags & EPI_RES) && primary) {
-          float rv[4];
-          load4(R + pix * p.ldr + co, rv);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] += rv[r];
-        }
-        if (flags & EPI_RELU) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
-        }
-        if (primary) store4(Y + pix * p.ldy + co, v);
-        else store4(Y2 + pix * p.ldy2 + (co - p.ysplit), v);
-      } else {
         for (int r = 0; r < 4; ++r) {
-          const int c = co + r;
-          if (c >= p.Cout) break;
-          float x = v[r];
-          if (flags & EPI_PRE_RELU) x = fmaxf(x, 0.f);
-          if (flags & EPI_AFFINE) x = (x - bnm[c]) * bni[c];
-          const bool primary = c < p.ysplit;
-          if ((flags & EPI_RES) && primary) x += (float)R[pix * p.ldr + c];
-          if (flags & EPI_RELU) x = fmaxf(x, 0.f);
-          if (primary) Y[pix * p.ldy + c] = (T)x;
-          else Y2[pix * p.ldy2 + (c - p.ysplit)] = (T)x;
+          const int idx = b0 + r * 256;
+          v[r] = make_uint4(0, 0, 0, 0);
+          if (idx < total) {
+            const int wp = idx / cu, u = idx - (idx / cu) * cu;
+            const int gp = gbase + wp;
+            if (gp >= 0 && gp < M) {
+              v[r] = *reinterpret_cast<const uint4*>(X + (size_t)gp * p.ldx + c0 + u * 8);
+              if (X2) {
+                bf16x8 a = __builtin_bit_cast(bf16x8, v[r]);
+                bf16x8 b = ld16(X2 + (size_t)gp * p.ldx2 + c0 + u * 8);
+                v[r] = __builtin_bit_cast(uint4, frag_add(a, b));
+              }
+            }
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int idx = b0 + r * 256;
+          if (idx < total) {
+            const int wp = idx / cu, u = idx - (idx / cu) * cu;
+            *reinterpret_cast<uint4*>(act + wp * p.win_astr + u * 16) = v[r];
+          }
         }
       }
     }
+    __syncthreads();
+    for (int k0 = 0; k0 < kcp; k0 += 32) {
+      const int4 t = ktab[(k0 >> 3) + (lane >> 4)];
+      bf16x8 a[WCO], b[WPX];
+#pragma unroll
+      for (int i = 0; i < WCO; ++i)
+        a[i] = *reinterpret_cast<const bf16x8*>(wts + (16 * i + col) * p.win_wstr +
+                                                (k0 + 8 * (lane >> 4)) * 2);
+#pragma unroll
+      for (int j = 0; j < WPX; ++j) {
+        const int y = hh[j] + t.z, x = ww[j] + t.w;
+        const bool ok = pv[j] && (unsigned)y < (unsigned)p.H && (unsigned)x < (unsigned)p.W;
+        b[j] = ok ? *reinterpret_cast<const bf16x8*>(act + (li[j] + t.x) * p.win_astr + t.y)
+                  : bf16x8{};
+      }
+#pragma unroll
+      for (int i = 0; i < WCO; ++i)
+#pragma unroll
+        for (int j = 0; j < WPX; ++j) acc[i][j] = mfma_step(a[i], b[j], acc[i][j]);
+    }
+    __syncthreads();
   }
+  conv_epilogue<bf16_t, WCO, WPX>(p, acc, pv, pbase, co0, 0, M);
+}
+
+template <int WCO, int WPX>
+static hipError_t launch_win_t(const ConvParams& p, hipStream_t s) {
+  const int M = p.N * p.H * p.W;
+  dim3 grid((M + 64 * WPX - 1) / (64 * WPX), p.cblocks, 1);
+  hipLaunchKernelGGL((conv_win<WCO, WPX>), grid, dim3(256), p.win_lds, s, p);
+  return hipGetLastError();
+}
+
+template <int WPX>
+static hipError_t launch_win_wco(const ConvParams& p, int wco, hipStream_t s) {
+  switch (wco) {
+    case 1: return launch_win_t<1, WPX>(p, s);
+    case 2: return launch_win_t<2, WPX>(p, s);
+    case 3: return launch_win_t<3, WPX>(p, s);
+    case 4: return launch_win_t<4, WPX>(p, s);
+    case 6: return launch_win_t<6, WPX>(p, s);
+    case 8: return launch_win_t<8, WPX>(p, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_conv_win(const ConvParams& p, const ConvLaunch& l, hipStream_t s) {
+  switch (l.wpx) {
+    case 1: return launch_win_wco<1>(p, l.wco, s);
+    case 2: return launch_win_wco<2>(p, l.wco, s);
+    case 4: return launch_win_wco<4>(p, l.wco, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+// ----------------------------------------------------------------------------
+// Register-resident 1x1 conv (any stride) for K = Cin <= 32*KS: a wave loads
+// its 16*WPX pixels' whole input vector into registers once (B fragments,
+// optional BN+ReLU prologue applied in registers), then sweeps every output
+// channel tile pair, WCO tiles (WCO/2 pairs) at a time, streaming weight
+// fragments from L1/L2.  Activations are read from HBM exactly once; no LDS.
+//
+// Paired-row weight layout (built on the host): within each 32-channel pair of
+// tiles (2q, 2q+1), MFMA row 4g+e of tile 2q+u holds output channel
+// 32q + 8g + 4u + e.  Lane group g = lane>>4 therefore ends up with 8
+// consecutive channels 32q+8g .. +7 of its pixel, so every epilogue access
+// (BN mean/inv, residual, output) is one 16-byte load/store per lane.  The
+// residual and BN operands of a tile group are fetched before its MFMAs.
+template <int KS, int WPX, int WCO>
+__global__ __launch_bounds__(256) void conv1x1_rr(ConvParams p) {
+  static_assert(WCO % 2 == 0, "paired tiles");
+  constexpr int NP = WCO / 2;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int col = lane & 15;
+  const int g = lane >> 4;
+  const int kl = g * 8;
+  const int M = p.N * p.Ho * p.Wo;
+  const int HoWo = p.Ho * p.Wo;
+  const int pbase = (blockIdx.x * 4 + wave) * (16 * WPX);
+  if (pbase >= M) return;
+  const bf16_t* __restrict__ X = reinterpret_cast<const bf16_t*>(p.x);
+  const bf16_t* __restrict__ Wt = reinterpret_cast<const bf16_t*>(p.w);
+  const bf16_t* __restrict__ R = reinterpret_cast<const bf16_t*>(p.res);
+  bf16_t* __restrict__ Y = reinterpret_cast<bf16_t*>(p.y);
+  bf16_t* __restrict__ Y2 = reinterpret_cast<bf16_t*>(p.y2);
+  const int flags = p.flags;
+
+  bool pv[WPX];
+  size_t pix[WPX];
+  bf16x8 b[KS][WPX];
+#pragma unroll
+  for (int j = 0; j < WPX; ++j) {
+    const int pp = pbase + 16 * j + col;
+    pv[j] = pp < M;
+    const int q = pv[j] ? pp : 0;
+    pix[j] = (size_t)q;
+    const int n = q / HoWo;
+    const int r = q - n * HoWo;
+    const int ho = r / p.Wo, wo = r - (r / p.Wo) * p.Wo;
+    const bf16_t* xp = X + (((size_t)n * p.H + ho * p.sh) * p.W + wo * p.sw) * p.ldx;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int c = s * 32 + kl;
+      b[s][j] = (pv[j] && c < p.Cin) ? ld16(xp + c) : bf16x8{};
+    }
+  }
+  if (p.in_mean) {
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int c = s * 32 + kl;
+      if (c < p.Cin) {
+        float im[8], ii[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { im[e] = p.in_mean[c + e]; ii[e] = p.in_inv[c + e]; }
+#pragma unroll
+        for (int j = 0; j < WPX; ++j)
+          if (pv[j]) b[s][j] = frag_bnrelu(b[s][j], im, ii);
+      }
+    }
+  }
+  const int tiles = p.coutp / 16;
+  const int per = ((tiles + gridDim.y - 1) / gridDim.y + WCO - 1) / WCO * WCO;
+  const int t0 = blockIdx.y * per, t1 = min(tiles, t0 + per);
+  for (int t = t0; t < t1; t += WCO) {
+    // epilogue operands first (independent of the MFMAs)
+    f32x4 bm[NP][2], bi[NP][2];
+    bf16x8 rv[NP][WPX];
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+      const int ch = (t / 2 + q) * 32 + 8 * g;
+      const bool cok = ch < p.Cout;
+      if ((flags & EPI_AFFINE) && cok) {
+        bm[q][0] = *reinterpret_cast<const f32x4*>(p.mean + ch);
+        bm[q][1] = *reinterpret_cast<const f32x4*>(p.mean + ch + 4);
+        bi[q][0] = *reinterpret_cast<const f32x4*>(p.inv + ch);
+        bi[q][1] = *reinterpret_cast<const f32x4*>(p.inv + ch + 4);
+      }
+#pragma unroll
+      for (int j = 0; j < WPX; ++j)
+        rv[q][j] = ((flags & EPI_RES) && cok && pv[j] && ch < p.ysplit)
+                       ? ld16(R + pix[j] * p.ldr + ch) : bf16x8{};
+    }
+    f32x4 acc[WCO][WPX];
+#pragma unroll
+    for (int i = 0; i < WCO; ++i)
+#pragma unroll
+      for (int j = 0; j < WPX; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      bf16x8 a[WCO];
+#pragma unroll
+      for (int i = 0; i < WCO; ++i) {
+        const int row = min(t + i, tiles - 1) * 16 + col;
+        a[i] = ld16(Wt + (size_t)row * p.kp + s * 32 + kl);
+      }
+#pragma unroll
+      for (int i = 0; i < WCO; ++i)
+#pragma unroll
+        for (int j = 0; j < WPX; ++j) acc[i][j] = mfma_step(a[i], b[s][j], acc[i][j]);
+    }
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+      const int ch = (t / 2 + q) * 32 + 8 * g;
+      if (ch >= p.Cout) continue;
+#pragma unroll
+      for (int j = 0; j < WPX; ++j) {
+        if (!pv[j]) continue;
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = acc[2 * q][j][e];
+          v[4 + e] = acc[2 * q + 1][j][e];
+        }
+        if (flags & EPI_PRE_RELU) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+        }
+        if (flags & EPI_AFFINE) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[e] = (v[e] - bm[q][0][e]) * bi[q][0][e];
+            v[4 + e] = (v[4 + e] - bm[q][1][e]) * bi[q][1][e];
+          }
+        }
+        if (flags & EPI_RES) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += (float)rv[q][j][e];
+        }
+        if (flags & EPI_RELU) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+        }
+        bf16x8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = (bf16_t)v[e];
+        bf16_t* dst = ch < p.ysplit ? Y + pix[j] * p.ldy + ch : Y2 + pix[j] * p.ldy2 + (ch - p.ysplit);
+        *reinterpret_cast<uint4*>(dst) = __builtin_bit_cast(uint4, o);
+      }
+    }
+  }
+}
+
+template <int KS, int WPX>
+static hipError_t launch_rr_t(const ConvParams& p, int wco, int ysplit_blocks, hipStream_t s) {
+  const int M = p.N * p.Ho * p.Wo;
+  dim3 grid((M + 64 * WPX - 1) / (64 * WPX), ysplit_blocks, 1);
+  if (wco == 4)
+    hipLaunchKernelGGL((conv1x1_rr<KS, WPX, 4>), grid, dim3(256), 0, s, p);
+  else
+    hipLaunchKernelGGL((conv1x1_rr<KS, WPX, 2>), grid, dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+int conv1x1_rr_max_wpx(int ks) {
+  // keep the B fragments (KS*WPX*4 VGPRs) within ~128 registers
+  if (ks <= 8) return 4;
+  if (ks <= 16) return 2;
+  return 1;
+}
+
+hipError_t launch_conv1x1_rr(const ConvParams& p, const ConvLaunch& l, hipStream_t s) {
+  const int ks = (p.cinp + 31) / 32;
+  const int ys = l.splitk > 0 ? l.splitk : 1;  // reused as the cout-split count
+#define RR_CASE(K)                                                        \
+  case K:                                                                 \
+    return l.wpx == 4 ? launch_rr_t<K, 4>(p, l.wco, ys, s)                \
+                      : (l.wpx == 2 ? launch_rr_t<K, 2>(p, l.wco, ys, s)  \
+                                    : launch_rr_t<K, 1>(p, l.wco, ys, s));
+#define RR_CASE2(K)                                                       \
+  case K:                                                                 \
+    return l.wpx == 2 ? launch_rr_t<K, 2>(p, l.wco, ys, s)                \
+                      : launch_rr_t<K, 1>(p, l.wco, ys, s);
+#define RR_CASE1(K) \
+  case K:           \
+    return launch_rr_t<K, 1>(p, l.wco, ys, s);
+  switch (ks) {
+    RR_CASE(1)
+    RR_CASE(2)
+    RR_CASE(3)
+    RR_CASE(4)
+    RR_CASE(6)
+    RR_CASE(8)
+    RR_CASE2(12)
+    RR_CASE2(16)
+    RR_CASE1(24)
+    RR_CASE1(32)
+  }
+#undef RR_CASE
+#undef RR_CASE2
+#undef RR_CASE1
+  return hipErrorInvalidValue;
+}
+
+// ----------------------------------------------------------------------------
+// LDS-tiled GEMM for compute-bound 1x1 convs (K = cinp % 64 == 0, any stride):
+// block tile 128 output channels x 128 pixels, BK = 64, 4 waves in 2x2, each
+// wave 64x64 = 4x4 MFMA 16x16x32 tiles.  Both operands are K-contiguous rows
+// staged global -> registers -> LDS (double-buffered; the next tile's global
+// loads are issued before the current tile's MFMAs).  LDS rows are 128 B with
+// 16-B chunk c of row r stored at chunk c ^ ((r>>1)&7): every ds_read_b128
+// lane group (rows 0-3,12-15 at chunk c, rows 4-11 at c+1) then covers all
+// 64 banks exactly once.  Weights use the paired-row layout so the epilogue
+// does 16-byte accesses (see conv1x1_rr).
+__device__ __forceinline__ int swz(int r, int c) { return r * 64 + ((c ^ ((r >> 1) & 7)) << 3); }
+
+__global__ __launch_bounds__(256) void gemm1x1_lds(ConvParams p) {
+  __shared__ __attribute__((aligned(16))) bf16_t As[2][128 * 64];
+  __shared__ __attribute__((aligned(16))) bf16_t Bs[2][128 * 64];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int col = lane & 15, g = lane >> 4;
+  const int M = p.N * p.Ho * p.Wo;
+  const int HoWo = p.Ho * p.Wo;
+  const int co0 = blockIdx.y * 128;
+  const int px0 = blockIdx.x * 128;
+  const bf16_t* __restrict__ X = reinterpret_cast<const bf16_t*>(p.x);
+  const bf16_t* __restrict__ Wt = reinterpret_cast<const bf16_t*>(p.w);
+  // staging assignment: 1024 16-B chunks per operand tile, 4 per thread
+  const bf16_t* ga[4];
+  const bf16_t* gb[4];
+  int lr[4], lc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = tid + 256 * i;
+    lr[i] = c >> 3;
+    lc[i] = c & 7;
+    ga[i] = Wt + (size_t)(co0 + lr[i]) * p.kp + lc[i] * 8;
+    const int pix = px0 + lr[i];
+    if (pix < M) {
+      const int n = pix / HoWo, r = pix - (pix / HoWo) * HoWo;
+      const int ho = r / p.Wo, wo = r - (r / p.Wo) * p.Wo;
+      gb[i] = X + (((size_t)n * p.H + ho * p.sh) * p.W + wo * p.sw) * p.ldx + lc[i] * 8;
+    } else {
+      gb[i] = nullptr;
+    }
+  }
+  uint4 ra[4], rb[4];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      ra[i] = *reinterpret_cast<const uint4*>(ga[i] + k0);
+      rb[i] = gb[i] ? *reinterpret_cast<const uint4*>(gb[i] + k0) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      *reinterpret_cast<uint4*>(&As[buf][swz(lr[i], lc[i])]) = ra[i];
+      *reinterpret_cast<uint4*>(&Bs[buf][swz(lr[i], lc[i])]) = rb[i];
+    }
+  };
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int KT = p.kp / 64;
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int kt = 0; kt < KT; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < KT) gload((kt + 1) * 64);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int c = ks * 4 + g;
+      bf16x8 a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        a[i] = *reinterpret_cast<const bf16x8*>(&As[cur][swz(wm * 64 + 16 * i + col, c)]);
+        b[i] = *reinterpret_cast<const bf16x8*>(&Bs[cur][swz(wn * 64 + 16 * i + col, c)]);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma_step(a[i], b[j], acc[i][j]);
+    }
+    if (kt + 1 < KT) lstore(cur ^ 1);
+    __syncthreads();
+  }
+
+  // paired epilogue: m-tiles (2q, 2q+1) of this wave -> 8 consecutive channels
+  const bf16_t* __restrict__ R = reinterpret_cast<const bf16_t*>(p.res);
+  bf16_t* __restrict__ Y = reinterpret_cast<bf16_t*>(p.y);
+  bf16_t* __restrict__ Y2 = reinterpret_cast<bf16_t*>(p.y2);
+  const int flags = p.flags;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int ch = co0 + wm * 64 + 32 * q + 8 * g;
+    if (ch >= p.Cout) continue;
+    f32x4 bm0, bm1, bi0, bi1;
+    if (flags & EPI_AFFINE) {
+      bm0 = *reinterpret_cast<const f32x4*>(p.mean + ch);
+      bm1 = *reinterpret_cast<const f32x4*>(p.mean + ch + 4);
+      bi0 = *reinterpret_cast<const f32x4*>(p.inv + ch);
+      bi1 = *reinterpret_cast<const f32x4*>(p.inv + ch + 4);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int pix = px0 + wn * 64 + 16 * j + col;
+      if (pix >= M) continue;
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = acc[2 * q][j][e];
+        v[4 + e] = acc[2 * q + 1][j][e];
+      }
+      if (flags & EPI_PRE_RELU) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+      }
+      if (flags & EPI_AFFINE) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = (v[e] - bm0[e]) * bi0[e];
+          v[4 + e] = (v[4 + e] - bm1[e]) * bi1[e];
+        }
+      }
+      if ((flags & EPI_RES) && ch < p.ysplit) {
+        bf16x8 rv = ld16(R + (size_t)pix * p.ldr + ch);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += (float)rv[e];
+      }
+      if (flags & EPI_RELU) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+      }
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = (bf16_t)v[e];
+      bf16_t* dst = ch < p.ysplit ? Y + (size_t)pix * p.ldy + ch
+                                  : Y2 + (size_t)pix * p.ldy2 + (ch - p.ysplit);
+      *reinterpret_cast<uint4*>(dst) = __builtin_bit_cast(uint4, o);
+    }
+  }
+}
+
+hipError_t launch_gemm1x1(const ConvParams& p, hipStream_t s) {
+  const int M = p.N * p.Ho * p.Wo;
+  dim3 grid((M + 127) / 128, p.coutp / 128, 1);
+  hipLaunchKernelGGL(gemm1x1_lds, grid, dim3(256), 0, s, p);
+  return hipGetLastError();
 }
 
 int conv_kstep(DType t) { return t == BF16 ? Tr<bf16_t>::KSTEP : Tr<float>::KSTEP; }

@@ -116,6 +116,14 @@ class Extractor:
             kind.ctypes.data_as(C.POINTER(C.c_int)), max_ops, C.c_void_p(sh)))
         return dict(ms=ms[:nops], flops=fl[:nops], bytes=by[:nops], kind=kind[:nops])
 
+    def describe(self, x):
+        """One line per kernel launch of the plan for x's shape."""
+        n, t, f = x.shape
+        need = check(lib().vox_plan_describe(self._h, C.c_void_p(x.data_ptr()), n, t, f, None, 0))
+        buf = C.create_string_buffer(need)
+        check(lib().vox_plan_describe(self._h, C.c_void_p(x.data_ptr()), n, t, f, buf, need))
+        return buf.value.decode().strip().split("\n")
+
     # -- tf_extract chunk loop ---------------------------------------------
     def embed_utterance(self, feat):
         feat = np.ascontiguousarray(feat, dtype=np.float32)
