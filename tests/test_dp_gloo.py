@@ -1,0 +1,69 @@
+"""The N>1 extraction path on CPU: 2 ranks over gloo, split_scp shards,
+variable-size all-gather, merged ark == `cat` of the per-rank arks
+(eval_inference_model.sh:38-39), cohort speaker means on rank 0."""
+
+import os
+import socket
+
+import numpy as np
+import pytest
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _fake_embed(x):
+    # deterministic per-utterance "embedding": depends only on that utterance
+    return np.concatenate([x.mean(1), x.std(1)], axis=1).astype(np.float32)[:, :8]
+
+
+def _items(n_utts):
+    rng = np.random.default_rng(0)
+    lens = rng.integers(25, 1300, size=n_utts)
+    feats = [(f"spk{i % 3}-u{i:03d}", rng.standard_normal((int(L), 4)).astype(np.float32))
+             for i, L in enumerate(lens)]
+
+    def items(rank, world):
+        from voxsrc2020_speaker_verification_amd.partition import shard
+        return shard(feats, rank, world)
+    return feats, items
+
+
+def _worker(rank, world, port, outdir, n_utts):
+    import torch.distributed as dist
+    from voxsrc2020_speaker_verification_amd import dp_extract
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    _, items = _items(n_utts)
+    spk2utt = os.path.join(outdir, "spk2utt")
+    dp_extract.run(rank, world, items, _fake_embed, 8, os.path.join(outdir, "xvector"),
+                   batch=3, cohort_spk2utt=spk2utt)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n_utts", [(2, 11), (3, 7)])
+def test_dp_extract_gloo(tmp_path, world, n_utts):
+    import torch.multiprocessing as mp
+    from voxsrc2020_speaker_verification_amd import kaldi
+    from voxsrc2020_speaker_verification_amd.extract import embed_utterances
+    feats, _ = _items(n_utts)
+    with open(tmp_path / "spk2utt", "w") as f:
+        for s in range(3):
+            f.write(f"spk{s} " + " ".join(k for k, _ in feats if k.startswith(f"spk{s}-")) + "\n")
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), n_utts), nprocs=world, join=True)
+    # merged ark is byte-identical to the concatenation of the per-rank arks
+    cat = b"".join(open(tmp_path / f"xvector.{r + 1}.ark", "rb").read() for r in range(world))
+    assert open(tmp_path / "xvector.ark", "rb").read() == cat
+    got = dict(kaldi.read_vec_flt_ark(str(tmp_path / "xvector.ark")))
+    assert list(got) == [k for k, _ in feats]
+    exp = embed_utterances(feats, _fake_embed, 8, batch=5)
+    for (k, _), e in zip(feats, exp):
+        np.testing.assert_array_equal(got[k], e)
+    coh = np.load(tmp_path / "xvector.cohort.npy")
+    assert coh.shape == (3, 8)

@@ -1,0 +1,101 @@
+"""The numpy oracle against an independent torch-CPU implementation
+(voxsrc2020_speaker_verification_amd.synth.torch_forward: NCHW, F.conv2d with
+explicit TF pads) for every backbone family, plus the TF padding/pooling rules
+of SURVEY.md Appendix A.  TF1 itself is not available: parity unpinned vs TF."""
+
+import io
+
+import numpy as np
+import pytest
+
+from oracle import models_ref as R
+
+
+@pytest.mark.parametrize("name,F,T,N", [
+    ("tdnn", 40, 60, 3),
+    ("tdnn", 80, 33, 2),
+    ("res2net50_w8_s6_c16", 24, 40, 2),
+    ("res2net50_w24_s4_c32", 16, 29, 2),
+    ("dpn68", 16, 27, 2),
+])
+def test_oracle_matches_torch(weights, name, F, T, N):
+    from voxsrc2020_speaker_verification_amd import synth
+    spec, t, blob = weights(name, F)
+    x = synth.make_features(N, T, F, seed=5)
+    a = R.forward(spec, t, x)
+    b = synth.torch_forward(spec, t, x)
+    assert a.shape == (N, spec["output_dim"])
+    assert np.abs(a - b).max() <= 1e-4 * np.abs(b).max()
+
+
+def test_tf_same_padding_rules():
+    assert R.tf_same_pads(200, 5, 1, 1) == (2, 2)      # TDNN k5
+    assert R.tf_same_pads(200, 3, 1, 2) == (2, 2)      # k3 d2
+    assert R.tf_same_pads(200, 3, 1, 3) == (3, 3)      # k3 d3
+    assert R.tf_same_pads(80, 3, 2) == (0, 1)          # DPN stride-2, even
+    assert R.tf_same_pads(75, 3, 2) == (1, 1)          # odd
+    assert R.tf_same_pads(80, 1, 2) == (0, 0)
+
+
+def test_fixed_padding_stride2_and_avgpool():
+    x = np.arange(2 * 5 * 4 * 3, dtype=np.float32).reshape(2, 5, 4, 3)
+    w = np.zeros((3, 3, 3, 3), np.float32)
+    w[1, 1, np.arange(3), np.arange(3)] = 1           # centre tap identity
+    y = R.conv2d_fixed_padding(x, w, 2)
+    assert y.shape == (2, 3, 2, 3)                     # ceil(H/2), ceil(W/2)
+    np.testing.assert_array_equal(y, x[:, ::2, ::2, :])
+    p = R.avg_pool3x3s2_valid(np.pad(np.ones((1, 4, 4, 1), np.float32), ((0, 0), (1, 1), (1, 1), (0, 0))))
+    assert p[0, 0, 0, 0] == pytest.approx(4 / 9)       # padded zeros counted, divisor 9
+
+
+def test_stats_pool_and_flatten_layout():
+    rng = np.random.default_rng(0)
+    x = rng.standard_normal((2, 7, 3, 4)).astype(np.float32)
+    f = R.flatten_nhwc(R.stats_pool(x))
+    assert f.shape == (2, 3 * 8)
+    w, c = 2, 1
+    np.testing.assert_allclose(f[:, w * 8 + c], x[:, :, w, c].mean(1), rtol=1e-6)
+    np.testing.assert_allclose(f[:, w * 8 + 4 + c], np.sqrt(x[:, :, w, c].var(1) + 1e-5), rtol=1e-5)
+
+
+def test_chunk_rule_table():
+    """tf_extract.py:102-107 on the boundary lengths of SURVEY.md §4."""
+    from voxsrc2020_speaker_verification_amd.extractor import chunk_plan
+    table = {25: [(0, 25)], 200: [(0, 200)], 999: [(0, 999)], 1000: [(0, 1000)],
+             1010: [(0, 1000)], 1024: [(0, 1000)], 1025: [(0, 1000), (1000, 25)],
+             2020: [(0, 1000), (1000, 1000)], 2025: [(0, 1000), (1000, 1000), (2000, 25)],
+             24: [], 1: []}
+    for T, plan in table.items():
+        assert chunk_plan(T) == plan, T
+
+
+def test_embed_utterances_matches_oracle_chunking(weights):
+    """Length-bucketed batching + chunk averaging == per-utterance reference loop."""
+    from voxsrc2020_speaker_verification_amd import synth
+    from voxsrc2020_speaker_verification_amd.extract import embed_utterances
+    spec, t, blob = weights("tdnn", 40)
+    rng = np.random.default_rng(1)
+    feats = [(f"u{i}", synth.make_features(1, T, 40, seed=i)[0])
+             for i, T in enumerate([30, 1030, 57, 1030, 2040, 25])]
+    got = embed_utterances(feats, lambda x: R.forward(spec, t, x), 256, batch=2)
+    for (k, f), g in zip(feats, got):
+        np.testing.assert_allclose(g, R.embed_utterance(spec, t, f), rtol=1e-5, atol=1e-5)
+    with pytest.raises(ZeroDivisionError):
+        embed_utterances([("short", np.zeros((24, 40), np.float32))], None, 256)
+
+
+def test_weight_blob_roundtrip_and_param_counts(weights):
+    from voxsrc2020_speaker_verification_amd import archs
+    from voxsrc2020_speaker_verification_amd import weights as W
+    spec, t, blob = weights("tdnn", 40)
+    spec2, t2 = W.load_blob(blob)
+    assert spec2 == {k: v for k, v in spec.items()}
+    assert list(t2) == list(t) and all(np.array_equal(t[k], t2[k]) for k in t)
+    # README.md:190,241-262 parameter counts (code recount)
+    counts = {("tdnn", 40): 3.51, ("res2net50_w24_s4_c32", 80): 17.73,
+              ("res2net50_w24_s4_c64", 80): 32.07, ("res2net50_w8_s6_c16", 80): 4.78,
+              ("dpn68", 80): 15.97, ("dpn68", 40): 13.84}
+    for (name, F), m in counts.items():
+        assert archs.param_count(archs.get_arch(name, F)) / 1e6 == pytest.approx(m, abs=0.006)
+    with pytest.raises(ValueError):
+        W.load_blob(b"NOTABLOB" + bytes(64))

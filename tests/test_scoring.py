@@ -1,0 +1,79 @@
+"""snorm.py / eer_minDCF.py / utt2id.py / split_scp.pl parity against golden
+fixtures generated from the reference itself."""
+
+import json
+import os
+
+import numpy as np
+import pytest
+
+G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def test_snorm_cosine_and_asnorm_match_reference():
+    from voxsrc2020_speaker_verification_amd import scoring as S
+    exp = np.load(os.path.join(G, "snorm_expected.npz"))
+    tx = S.read_xvector(os.path.join(G, "snorm_test.ark"))
+    cos = S.cosine_scores(tx, os.path.join(G, "snorm_trials.txt"))
+    assert np.array_equal(np.array([s for *_, s in cos], np.float64), exp["cosine"])
+    coh = S.cohort_xvectors(os.path.join(G, "snorm_cohort.ark"), os.path.join(G, "snorm_spk2utt"))
+    assert list(coh) == list(exp["cohort_keys"])
+    assert np.array_equal(np.array(list(coh.values())), exp["cohort"])
+    m, s = S.cohort_mean_std(tx, coh)
+    keys = list(exp["test_keys"])
+    assert np.array_equal(np.array([m[k] for k in keys]), exp["mean"])
+    assert np.array_equal(np.array([s[k] for k in keys]), exp["std"])
+    asn = S.asnorm_scores(m, s, cos)
+    assert np.array_equal(np.array([v for *_, v in asn], np.float64), exp["asnorm"])
+
+
+@pytest.mark.parametrize("case", ["small", "ties", "large"])
+def test_eer_min_dcf_match_reference(case):
+    from voxsrc2020_speaker_verification_amd.scoring import compute_eer_and_min_dcf
+    c = json.load(open(os.path.join(G, "eer_cases.json")))[case]
+    eer, thr, mindcf, mthr = compute_eer_and_min_dcf(c["y"], c["s"], 1, 1, 0.01)
+    assert eer == c["eer"] and thr == c["eer_threshold"]
+    assert mindcf == c["min_dcf"] and mthr == c["min_dcf_threshold"]
+
+
+def test_utt2id_bit_exact(tmp_path):
+    from voxsrc2020_speaker_verification_amd.scoring import utt2id_main
+    c = json.load(open(os.path.join(G, "utt2id_cases.json")))
+    for n, text in c["files"].items():
+        (tmp_path / n).write_text(text)
+    p = lambda n: str(tmp_path / n)  # noqa: E731
+    got = utt2id_main(["utt2id.py", p("utt2spk_a"), p("spk_a"), "out.pkl"])
+    assert got == c["one_pair"]
+    assert list(got.items()) == list(c["one_pair"].items())
+    assert c["two_pairs_error"] == "ValueError"
+    with pytest.raises(ValueError):
+        utt2id_main(["utt2id.py", p("utt2spk_a"), p("spk_a"), p("utt2spk_b"), p("spk_b"), "o"])
+
+
+def test_split_scp_shards_match_perl():
+    from voxsrc2020_speaker_verification_amd.partition import shard_bounds
+    cases = json.load(open(os.path.join(G, "split_scp_cases.json")))
+    for key, shards in cases.items():
+        n, N = map(int, key.split("_"))
+        names = [f"utt{i:04d}" for i in range(n)]
+        assert [names[b:e] for b, e in shard_bounds(n, N)] == shards
+    with pytest.raises(ValueError):
+        shard_bounds(3, 4)
+    with pytest.raises(ValueError):
+        shard_bounds(0, 1)
+
+
+def test_cli_mirrors(tmp_path, capsys):
+    """snorm / eer_minDCF command lines write the reference's files and lines."""
+    from voxsrc2020_speaker_verification_amd import eer_minDCF, snorm
+    exp = np.load(os.path.join(G, "snorm_expected.npz"))
+    cos, asn = tmp_path / "cos.txt", tmp_path / "asn.txt"
+    snorm.main(["--trial", os.path.join(G, "snorm_trials.txt"),
+                "--test_ark", os.path.join(G, "snorm_test.ark"), "--cosine_score", str(cos),
+                "--cohort_ark", os.path.join(G, "snorm_cohort.ark"),
+                "--cohort_spk2utt", os.path.join(G, "snorm_spk2utt"), "--snorm_score", str(asn)])
+    vals = [float(l.split()[2]) for l in open(asn)]
+    np.testing.assert_allclose(vals, exp["asnorm"], rtol=1e-6)
+    eer_minDCF.main(["--trial", os.path.join(G, "snorm_trials.txt"), "--score", str(cos)])
+    out = capsys.readouterr().out
+    assert out.startswith("EER is ") and "minDCF is " in out

@@ -1,0 +1,127 @@
+"""Data-parallel extraction: one process per GPU + one RCCL all-gather.
+
+Reference: tensorflow/eval_inference_model.sh:27-40 starts `num_gpus`
+independent tf_extract.py processes (CUDA_VISIBLE_DEVICES=i-1) on the
+contiguous shards data/<set>/<N>-split/feats.<i>.scp and then "gathers" with
+`cat xvector.{1..N}.ark > xvector.ark`.  Here each rank extracts the
+split_scp.pl shard of the scp (or reads the reference's pre-split shard
+file), then the per-rank embedding matrices are assembled on every rank with
+one all-gather over RCCL/xGMI (backend "nccl"; "gloo" for CPU tests).  Rank 0
+writes the merged ark/scp in shard order, i.e. byte-identical to the `cat`,
+plus (optionally) the cohort speaker-mean matrix for AS-norm (snorm.py:45-67).
+
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 -m \\
+        voxsrc2020_speaker_verification_amd.dp_extract --pb-file m.blob \\
+        --rspec data/voxceleb2_dev/fbank80 --wspec exp/emb/voxceleb2_dev/xvector \\
+        --cohort-spk2utt data/voxceleb2_dev/spk2utt
+"""
+
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+
+import numpy as np
+
+
+def gather_embeddings(keys, emb, group=None, device=None):
+    """All-gather variable-sized [n_r, D] float32 matrices (+ their keys) from
+    every rank; returns (all_keys, [sum n_r, D]) in rank order."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    dim = emb.shape[1]
+    dev = device if device is not None else torch.device("cpu")
+    n = torch.tensor([emb.shape[0]], dtype=torch.int64, device=dev)
+    counts = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(counts, n, group=group)
+    counts = [int(c.item()) for c in counts]
+    mx = max(counts)
+    buf = torch.zeros((mx, dim), dtype=torch.float32, device=dev)
+    if emb.shape[0]:
+        buf[:emb.shape[0]] = torch.from_numpy(np.ascontiguousarray(emb)).to(dev)
+    parts = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(parts, buf, group=group)
+    key_lists = [None] * world
+    dist.all_gather_object(key_lists, list(keys), group=group)
+    mats = [p[:c].cpu().numpy() for p, c in zip(parts, counts)]
+    all_keys = [k for kl in key_lists for k in kl]
+    return all_keys, (np.concatenate(mats, 0) if mats else np.zeros((0, dim), np.float32))
+
+
+def run(rank, world, scp_items, embed_fn, dim, wspec, shard_file=None, batch=64,
+        device=None, write_per_rank=True, cohort_spk2utt=None):
+    """The per-rank body (also used by the gloo tests with a fake embedder).
+    scp_items: full list of (key, feat) is NOT required -- each rank only
+    decodes its own shard: `scp_items` is a callable(rank, world) -> list of
+    (key, [T,F] features)."""
+    from .extract import embed_utterances, write_vectors
+    feats = scp_items(rank, world)
+    emb = embed_utterances(feats, embed_fn, dim, batch) if feats else np.zeros((0, dim), np.float32)
+    keys = [k for k, _ in feats]
+    if write_per_rank and wspec:
+        write_vectors(f"{wspec}.{rank + 1}", keys, emb)   # xvector.<i>.ark as the reference
+    all_keys, all_emb = gather_embeddings(keys, emb, device=device)
+    if rank == 0 and wspec:
+        write_vectors(wspec, all_keys, all_emb)           # == cat xvector.{1..N}.ark
+        if cohort_spk2utt:
+            from .scoring import l2norm, read_spk2utt, speaker_xvectors
+            xv = {k: l2norm(v, axis=0) for k, v in zip(all_keys, all_emb)}
+            spk = speaker_xvectors(xv, read_spk2utt(cohort_spk2utt))
+            np.save(wspec + ".cohort.npy", np.array(list(spk.values()), np.float32))
+            with open(wspec + ".cohort.keys", "w") as f:
+                f.write("\n".join(spk) + "\n")
+    return all_keys, all_emb
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--pb-file", dest="pb_file", required=True)
+    ap.add_argument("--rspec", required=True, help="<base> of <base>.scp (sharded here) or, "
+                    "with --pre-split, the shard template '<dir>/feats' (feats.<i>.scp)")
+    ap.add_argument("--pre-split", action="store_true")
+    ap.add_argument("--wspec", required=True)
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--cohort-spk2utt", default=None)
+    a = ap.parse_args(argv)
+
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29533")
+    torch.cuda.set_device(local)
+    dist.init_process_group("nccl", rank=rank, world_size=world,
+                            device_id=torch.device("cuda", local))
+    from .extractor import Extractor
+    from .kaldi import iter_features
+    from .partition import shard
+
+    def items(r, w):
+        if a.pre_split:
+            return list(iter_features(f"{a.rspec}.{r + 1}.scp"))
+        from .kaldi import parse_rxfile, read_mat, read_scp, sliding_cmn
+        lines = shard(read_scp(a.rspec + ".scp"), r, w)
+        out = []
+        for key, rx in lines:
+            path, off, rng = parse_rxfile(rx)
+            m = read_mat(path, off)
+            if rng is not None:
+                m = np.ascontiguousarray(m[rng])
+            out.append((key, sliding_cmn(m)))
+        return out
+
+    with Extractor(a.pb_file, device=local, precision=a.precision) as ex:
+        run(rank, world, items, ex.run, ex.dim, a.wspec, batch=a.batch,
+            device=torch.device("cuda", local), cohort_spk2utt=a.cohort_spk2utt)
+    dist.barrier()
+    dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

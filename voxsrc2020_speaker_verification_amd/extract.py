@@ -1,0 +1,98 @@
+"""`tf_extract.py` drop-in: FBANK scp in -> sliding CMN -> backbone -> FV ark+scp out.
+
+Reference: tensorflow/tf_extract.py:45-113.  Same flags (--pb-file,
+--expand-dim, --rspec <base> (reads <base>.scp), --wspec <base> (writes
+<base>.ark/.scp)), same chunk rule (:96-111), same output bytes.  Differences,
+all result-preserving:
+  * chunks of equal length are batched together (the reference runs batch 1,
+    :27); embeddings are batch-independent (bitwise, tests/test_gpu_parity.py);
+  * no reader process / pickle queue: features are decoded natively;
+  * --pb-file takes a VOXEMB01 weight blob (see weights.py / INTEGRATION.md);
+  * an utterance shorter than 25 frames raises ZeroDivisionError, as the
+    reference does at :111, before anything is written for later utterances.
+
+    python -m voxsrc2020_speaker_verification_amd.extract --pb-file m.blob \\
+        --expand-dim 3 --rspec data/voxceleb1/8-split/feats.1 --wspec out/xvector.1
+"""
+
+from __future__ import annotations
+
+import argparse
+import sys
+
+import numpy as np
+
+from .extractor import MIN_FRAMES, chunk_plan
+
+
+def embed_utterances(feats, embed_batch, dim, batch=64):
+    """feats: list of (key, [T,F] float32).  embed_batch(x[n,L,F]) -> [n,dim].
+    Returns [len(feats), dim] float32 in input order, applying the chunk rule
+    with chunks of equal length batched together."""
+    plans = []
+    buckets = {}
+    for u, (key, f) in enumerate(feats):
+        plan = chunk_plan(f.shape[0])
+        if not plan:
+            raise ZeroDivisionError(f"utterance {key} has {f.shape[0]} < {MIN_FRAMES} frames "
+                                    "(tf_extract.py:102,111)")
+        plans.append(plan)
+        for ci, (s, L) in enumerate(plan):
+            buckets.setdefault(L, []).append((u, ci, s))
+    chunk_emb = {}
+    for L, items in buckets.items():
+        for b in range(0, len(items), batch):
+            part = items[b:b + batch]
+            x = np.stack([feats[u][1][s:s + L] for (u, ci, s) in part])
+            e = embed_batch(x)
+            for (u, ci, s), row in zip(part, e):
+                chunk_emb[(u, ci)] = row
+    out = np.empty((len(feats), dim), np.float32)
+    for u, plan in enumerate(plans):
+        # target_values.append(value * length); sum(...) / sum(lengths) in float32
+        acc = 0
+        for ci, (s, L) in enumerate(plan):
+            acc = acc + chunk_emb[(u, ci)] * L
+        out[u] = acc / sum(L for _, L in plan)
+    return out
+
+
+def extract_scp(scp_path, embed_batch, dim, batch=64, cmn=True):
+    """(keys, embeddings) for every utterance of an scp, in scp order."""
+    from .kaldi import iter_features
+    feats = list(iter_features(scp_path, cmn=cmn))
+    return [k for k, _ in feats], embed_utterances(feats, embed_batch, dim, batch)
+
+
+def write_vectors(base, keys, emb):
+    from .kaldi import VectorWriter
+    with VectorWriter(base) as w:
+        for k, v in zip(keys, emb):
+            w.write(k, v)
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--pb-file", dest="pb_file", required=True,
+                    help="VOXEMB01 weight blob (converted from the frozen .pb)")
+    ap.add_argument("--expand-dim", dest="expand_dim", type=int, default=2,
+                    help="2 for 1-D conv models (TDNN), 3 for 2-D conv models")
+    ap.add_argument("--rspec", default="/tmp/fbank", help="fbank scp without '.scp'")
+    ap.add_argument("--wspec", default="/tmp/xvector", help="output ark/scp base")
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--device", type=int, default=0)
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--no-cmn", action="store_true", help="features are already CMN'd")
+    a = ap.parse_args(argv)
+    from .extractor import Extractor
+    with Extractor(a.pb_file, device=a.device, precision=a.precision) as ex:
+        if ex.expand_dim != a.expand_dim:
+            print(f"warning: --expand-dim {a.expand_dim} but the model layout is "
+                  f"{ex.expand_dim}; using the model's", file=sys.stderr)
+        keys, emb = extract_scp(a.rspec + ".scp", ex.run, ex.dim, a.batch, cmn=not a.no_cmn)
+    write_vectors(a.wspec, keys, emb)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,179 @@
+"""Kaldi table I/O for the extraction path, without Kaldi binaries.
+
+Replaces, for this path:
+  * the rspec pipe `ark:apply-cmvn-sliding --norm-vars=false --center=true
+    --cmn-window=300 scp:<rspec>.scp ark:- |` (tensorflow/tf_extract.py:63) ->
+    `iter_features(scp)`: scp parse, binary matrix read (FM/DM/CM), sliding CMN
+    (native, libvoxemb);
+  * the wspec pipe `ark:| copy-vector ark:- ark,scp:<wspec>.ark,<wspec>.scp`
+    (tf_extract.py:65) + kaldi_io.write_vec_flt (kaldi_io.py:304-334) ->
+    `VectorWriter`: FV records byte-identical to kaldi_io, plus the scp;
+  * kaldi_io.read_vec_flt_ark (kaldi_io.py:249-300) -> `read_vec_flt_ark`.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+import numpy as np
+
+from ._native import check, fptr, lib
+
+CMN_WINDOW = 300
+
+
+def read_scp(path):
+    """[(key, rxfile)] from a Kaldi scp (`key rxfile` per line)."""
+    out = []
+    with open(path, "r") as f:
+        for ln in f:
+            ln = ln.strip()
+            if not ln:
+                continue
+            key, rx = ln.split(None, 1)
+            out.append((key, rx))
+    return out
+
+
+_RANGE = re.compile(r"^(.+)\[(.+)\]$")
+
+
+def parse_rxfile(rx):
+    """'path:offset[range]' -> (path, offset, (row_slice, col_slice) or None)."""
+    rng = None
+    m = _RANGE.match(rx)
+    if m:
+        rx, r = m.group(1), m.group(2)
+        sl = []
+        for part in r.split(","):
+            a, b = part.split(":")
+            sl.append(slice(int(a) if a else None, int(b) + 1 if b else None))
+        rng = tuple(sl)
+    mo = re.search(r":([0-9]+)$", rx)
+    if mo:
+        return rx[:mo.start()], int(mo.group(1)), rng
+    return rx, 0, rng
+
+
+def read_mat(path, offset=0):
+    """Binary Kaldi matrix (FM / DM / CM) at `offset` -> float32 [rows, cols]."""
+    r, c = C.c_int(), C.c_int()
+    check(lib().vox_mat_shape(os.fsencode(path), int(offset), C.byref(r), C.byref(c)))
+    out = np.empty((r.value, c.value), np.float32)
+    check(lib().vox_read_mat(os.fsencode(path), int(offset), fptr(out), r.value, c.value))
+    return out
+
+
+def parse_mat(buf):
+    """Binary matrix from bytes starting at '\\0B' -> (float32 array, bytes used)."""
+    r, c = C.c_int(), C.c_int()
+    check(lib().vox_parse_mat_shape(buf, len(buf), C.byref(r), C.byref(c)))
+    out = np.empty((r.value, c.value), np.float32)
+    used = C.c_size_t()
+    check(lib().vox_parse_mat(buf, len(buf), fptr(out), r.value, c.value, C.byref(used)))
+    return out, used.value
+
+
+def _read_key(buf, pos):
+    end = buf.index(b" ", pos)
+    return buf[pos:end].decode("utf-8").strip(), end + 1
+
+
+def read_mat_ark(path):
+    """Generator of (key, matrix) over an ark of binary matrices (kaldi_io.read_mat_ark)."""
+    with open(path, "rb") as f:
+        buf = f.read()
+    pos = 0
+    while pos < len(buf):
+        key, pos = _read_key(buf, pos)
+        if not key:
+            break
+        mat, used = parse_mat(buf[pos:])
+        pos += used
+        yield key, mat
+
+
+def sliding_cmn(x, cmn_window=CMN_WINDOW, center=True):
+    """Kaldi apply-cmvn-sliding --norm-vars=false (double-precision running sums)."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    out = np.empty_like(x)
+    T, F = x.shape
+    check(lib().vox_sliding_cmn(fptr(x), T, F, int(cmn_window), 1 if center else 0, fptr(out)))
+    return out
+
+
+def iter_features(scp_path, cmn=True):
+    """(key, float32 [T, F]) in scp order: the tf_extract rspec pipeline."""
+    for key, rx in read_scp(scp_path):
+        path, off, rng = parse_rxfile(rx)
+        mat = read_mat(path, off)
+        if rng is not None:
+            mat = np.ascontiguousarray(mat[rng])
+        yield key, (sliding_cmn(mat) if cmn else mat)
+
+
+def format_vec_flt(key, v):
+    """Bytes of one FV ark record and the offset of its '\\0B' (for the scp)."""
+    v = np.ascontiguousarray(v, dtype=np.float32)
+    off = C.c_int64()
+    k = key.encode("utf-8")
+    need = lib().vox_format_vec_flt(k, fptr(v), v.shape[0], None, 0, C.byref(off))
+    check(need)
+    buf = C.create_string_buffer(need)
+    check(lib().vox_format_vec_flt(k, fptr(v), v.shape[0], buf, need, C.byref(off)))
+    return buf.raw[:need], off.value
+
+
+class VectorWriter:
+    """`ark,scp:<base>.ark,<base>.scp` writer of float vectors (copy-vector)."""
+
+    def __init__(self, base):
+        self.ark_path = base + ".ark"
+        self.scp_path = base + ".scp"
+        self._ark = open(self.ark_path, "wb")
+        self._scp = open(self.scp_path, "w")
+
+    def write(self, key, v):
+        rec, off = format_vec_flt(key, v)
+        pos = self._ark.tell()
+        self._ark.write(rec)
+        self._scp.write(f"{key} {self.ark_path}:{pos + off}\n")
+
+    def close(self):
+        if self._ark:
+            self._ark.close()
+            self._scp.close()
+            self._ark = self._scp = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
+def read_vec_flt_ark(path):
+    """Generator of (key, float32/float64 vector) over an FV/DV ark."""
+    with open(path, "rb") as f:
+        buf = f.read()
+    pos = 0
+    n = len(buf)
+    while pos < n:
+        key, pos = _read_key(buf, pos)
+        if not key:
+            break
+        if buf[pos:pos + 2] != b"\0B":
+            raise ValueError(f"{path}: only binary vectors are supported (key {key})")
+        hdr = buf[pos + 2:pos + 5]
+        if hdr == b"FV ":
+            dt, es = np.float32, 4
+        elif hdr == b"DV ":
+            dt, es = np.float64, 8
+        else:
+            raise ValueError(f"{path}: unknown vector header {hdr!r}")
+        dim = int(np.frombuffer(buf, np.int32, 1, pos + 6)[0])
+        start = pos + 10
+        yield key, np.frombuffer(buf, dt, dim, start).copy()
+        pos = start + dim * es

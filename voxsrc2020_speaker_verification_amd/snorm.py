@@ -1,0 +1,46 @@
+"""CLI mirror of tensorflow/snorm.py:134-182 (same flags, same output files).
+
+    python -m voxsrc2020_speaker_verification_amd.snorm --trial T --test_ark A \\
+        --cosine_score C [--cohort_ark X --cohort_spk2utt S | --weight_matrix W.npy] \\
+        [--snorm_score O] [--test_spk2utt S]
+"""
+
+import argparse
+import sys
+
+import numpy as np
+
+from . import scoring as S
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--test_ark", type=str)
+    ap.add_argument("--test_spk2utt", type=str, default=None)
+    ap.add_argument("--trial", type=str)
+    ap.add_argument("--cosine_score", type=str)
+    ap.add_argument("--cohort_ark", type=str, default=None)
+    ap.add_argument("--cohort_spk2utt", type=str, default=None)
+    ap.add_argument("--weight_matrix", type=str, default=None,
+                    help="projection matrix as .npy (the reference's .pkl is not unpickled)")
+    ap.add_argument("--snorm_score", type=str, default=None)
+    a = ap.parse_args(argv)
+    test = S.read_xvector(a.test_ark)
+    if a.test_spk2utt is not None:
+        test.update(S.speaker_xvectors(test, S.read_spk2utt(a.test_spk2utt)))
+    cos = S.cosine_scores(test, a.trial)
+    S.write_scores(a.cosine_score, cos)
+    if a.snorm_score is not None:
+        if a.cohort_ark is not None and a.cohort_spk2utt is not None:
+            cohort = S.cohort_xvectors(a.cohort_ark, a.cohort_spk2utt)
+        elif a.weight_matrix is not None:
+            cohort = S.projection_cohort(np.load(a.weight_matrix, allow_pickle=False))
+        else:
+            raise ValueError("Can not compute snorm scores: no cohort vectors provided")
+        m, s = S.cohort_mean_std(test, cohort)
+        S.write_scores(a.snorm_score, S.asnorm_scores(m, s, cos))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
