@@ -85,8 +85,11 @@ def conv2d_fixed_padding(x, w, stride):
     return conv2d(x, w, (stride, stride), (1, 1), ((pb, pe), (pb, pe)))
 
 
-def batch_norm(x, mean, var, eps=BN_EPS_4D):
-    """Inference BN with no gamma/beta (center=False, scale=False): models.py:62-67."""
+def batch_norm(x, mean, var, eps=None):
+    """Inference BN with no gamma/beta (center=False, scale=False): models.py:62-67.
+    eps defaults to the 4-D (fused) epsilon of the current blob."""
+    if eps is None:
+        eps = BN_EPS_4D
     inv = (np.float32(1.0) / np.sqrt(var.astype(np.float32) + np.float32(eps))).astype(np.float32)
     return ((x - mean.astype(np.float32)) * inv).astype(np.float32)
 
@@ -259,12 +262,19 @@ def dpn_forward(spec, tensors, x):
     return _head_tail(p, x)
 
 
+def _eps_from(spec):
+    global BN_EPS_4D, BN_EPS_2D
+    BN_EPS_4D = float(spec.get("bn_eps_4d", 1.001e-5))
+    BN_EPS_2D = float(spec.get("bn_eps_2d", 1e-5))
+
+
 def forward(spec, tensors, feats):
     """One `sess.run(outputs, {inputs: x})` (tf_extract.py:108).
 
     feats: [N, T, F] float32 (post-CMN FBANK).  The expand_dim rule of
     tf_extract.py:32 is applied here: TDNN -> [N,T,1,F], 2-D -> [N,T,F,1]."""
     feats = np.asarray(feats, np.float32)
+    _eps_from(spec)
     fam = spec["family"]
     if fam == "tdnn":
         return tdnn_forward(spec, tensors, feats[:, :, None, :])

@@ -138,3 +138,40 @@ def test_bad_inputs_fail_loudly(weights):
             ex.run(np.zeros((2, 50, 41), np.float32))   # wrong feature dim
         with pytest.raises(_native.VoxError):
             ex.run(np.zeros((0, 50, 40), np.float32))   # empty batch
+
+
+def _write_fm_ark(path, mats):
+    """Binary FM ark as kaldi_io.write_mat writes it; returns scp lines."""
+    import struct
+    lines = []
+    with open(path, "wb") as f:
+        for key, m in mats:
+            f.write(key.encode() + b" ")
+            off = f.tell()
+            f.write(b"\0BFM \x04" + struct.pack("<i", m.shape[0]) + b"\x04" +
+                    struct.pack("<i", m.shape[1]) + m.astype("<f4").tobytes())
+            lines.append(f"{key} {path}:{off}\n")
+    return lines
+
+
+def test_extract_cli_end_to_end(weights, tmp_path):
+    """scp -> sliding CMN -> chunked forward -> FV ark/scp, against the oracle
+    pipeline (oracle CMN + oracle chunk loop), fp32."""
+    from oracle import kaldi_ref, models_ref
+    from voxsrc2020_speaker_verification_amd import extract, kaldi, synth
+    spec, t, blob = weights("tdnn", 40)
+    (tmp_path / "m.blob").write_bytes(blob)
+    rng = np.random.default_rng(5)
+    mats = [(f"spk{i % 2}-utt{i}", (rng.standard_normal((T, 40)) * 3 + 5).astype(np.float32))
+            for i, T in enumerate([180, 1030, 333, 2100, 25])]
+    scp = _write_fm_ark(str(tmp_path / "feats.ark"), mats)
+    (tmp_path / "feats.scp").write_text("".join(scp))
+    extract.main(["--pb-file", str(tmp_path / "m.blob"), "--expand-dim", "2",
+                  "--rspec", str(tmp_path / "feats"), "--wspec", str(tmp_path / "xv"),
+                  "--precision", "fp32", "--batch", "3"])
+    got = dict(kaldi.read_vec_flt_ark(str(tmp_path / "xv.ark")))
+    assert list(got) == [k for k, _ in mats]
+    for k, m in mats:
+        ref = models_ref.embed_utterance(spec, t, kaldi_ref.sliding_cmn(m))
+        assert np.abs(got[k] - ref).max() <= 1e-3 * np.abs(ref).max(), k
+    assert len(open(tmp_path / "xv.scp").read().splitlines()) == len(mats)

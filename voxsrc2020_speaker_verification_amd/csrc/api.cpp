@@ -210,6 +210,7 @@ struct vox_model {
   float* plan_out = nullptr;
   std::vector<Op> plan;
   DevBuf stage_in, stage_out;  // host-API staging
+  float eps4 = 1.001e-5f, eps2 = 1e-5f;  // BN epsilons (blob header may override)
   bool no_win = false;         // VOXEMB_NO_WIN=1: disable conv_win (A/B testing)
   bool no_rr = false;          // VOXEMB_NO_RR=1: disable conv1x1_rr
   bool no_gemm = false;        // VOXEMB_NO_GEMM=1: disable gemm1x1_lds
@@ -348,24 +349,24 @@ static int load_weights(vox_model* m, const std::vector<HostTensor>& ts) {
   if (m->family == "tdnn") {
     for (size_t l = 0; l < m->spec.getv("filters").size(); ++l) {
       ConvW cw;
-      if ((rc = conv_bn(kEps4, cw))) return rc;
+      if ((rc = conv_bn(m->eps4, cw))) return rc;
       m->convs.push_back(cw);
     }
   } else if (m->family == "res2net") {
     const int s = m->spec.geti("split");
     auto blocks = m->spec.getv("block_sizes");
     ConvW stem;
-    if ((rc = conv_bn(kEps4, stem))) return rc;
+    if ((rc = conv_bn(m->eps4, stem))) return rc;
     m->convs.push_back(stem);
     for (size_t st = 0; st < blocks.size(); ++st)
       for (int b = 0; b < blocks[st]; ++b) {
         if (b == 0) {
           ConvW pr;
-          if ((rc = conv_bn(kEps4, pr))) return rc;
+          if ((rc = conv_bn(m->eps4, pr))) return rc;
           m->convs.push_back(pr);
         }
         ConvW a;
-        if ((rc = conv_bn(kEps4, a))) return rc;
+        if ((rc = conv_bn(m->eps4, a))) return rc;
         m->convs.push_back(a);
         NEXT(k, "split kernel");
         const int w = k->shape[2];
@@ -373,17 +374,17 @@ static int load_weights(vox_model* m, const std::vector<HostTensor>& ts) {
           NEXT(bm, "split bn mean");
           NEXT(bv, "split bn var");
           ConvW br;
-          if ((rc = make_conv(m, *k, 1, bm, bv, kEps4, dt, br, j * w, w))) return rc;
+          if ((rc = make_conv(m, *k, 1, bm, bv, m->eps4, dt, br, j * w, w))) return rc;
           m->convs.push_back(br);
         }
         ConvW c;
-        if ((rc = conv_bn(kEps4, c))) return rc;
+        if ((rc = conv_bn(m->eps4, c))) return rc;
         m->convs.push_back(c);
       }
   } else if (m->family == "dpn") {
     const int G = m->spec.geti("cardinality");
     ConvW stem;
-    if ((rc = conv_bn(kEps4, stem))) return rc;
+    if ((rc = conv_bn(m->eps4, stem))) return rc;
     m->convs.push_back(stem);
     // every body conv is BN->ReLU->conv: BN becomes the conv's prologue
     auto ks = m->spec.getv("k_sec");
@@ -395,18 +396,18 @@ static int load_weights(vox_model* m, const std::vector<HostTensor>& ts) {
           NEXT(bv, "bn var");
           NEXT(k, "conv");
           BNW pro;
-          if ((rc = make_bn(*bm, *bv, kEps4, pro))) return rc;
+          if ((rc = make_bn(*bm, *bv, m->eps4, pro))) return rc;
           m->bns.push_back(pro);
           ConvW cw;
           const int groups = (k->shape[0] == 3) ? G : 1;
-          if ((rc = make_conv(m, *k, groups, nullptr, nullptr, kEps4, dt, cw))) return rc;
+          if ((rc = make_conv(m, *k, groups, nullptr, nullptr, m->eps4, dt, cw))) return rc;
           m->convs.push_back(cw);
         }
       }
     NEXT(fm, "final bn mean");
     NEXT(fv, "final bn var");
     BNW fin;
-    if ((rc = make_bn(*fm, *fv, kEps4, fin))) return rc;
+    if ((rc = make_bn(*fm, *fv, m->eps4, fin))) return rc;
     m->bns.push_back(fin);
   } else {
     return fail(VOX_EINVAL, "unknown family " + m->family);
@@ -417,10 +418,10 @@ static int load_weights(vox_model* m, const std::vector<HostTensor>& ts) {
   NEXT(dk, "dense kernel");
   NEXT(h2m, "head bn2 mean");
   NEXT(h2v, "head bn2 var");
-  if ((rc = make_bn(*h1m, *h1v, kEps2, m->head_bn1))) return rc;
+  if ((rc = make_bn(*h1m, *h1v, m->eps2, m->head_bn1))) return rc;
   HostTensor dk4 = *dk;  // [D, out] -> HWIO [1,1,D,out]
   dk4.shape = {1, 1, dk->shape[0], dk->shape[1]};
-  if ((rc = make_conv(m, dk4, 1, h2m, h2v, kEps2, F32, m->head))) return rc;
+  if ((rc = make_conv(m, dk4, 1, h2m, h2v, m->eps2, F32, m->head))) return rc;
   m->pooled = dk->shape[0];
   m->out_dim = dk->shape[1];
   if (cur.i != ts.size()) return fail(VOX_EIO, "blob has trailing tensors");
@@ -874,6 +875,8 @@ extern "C" int vox_load_blob(const void* blob, size_t nbytes, int device, int pr
   m->family = spec.get("family");
   m->feat_dim = spec.geti("feat_dim");
   m->expand_dim = spec.geti("expand_dim", 3);
+  if (!spec.get("bn_eps_4d").empty()) m->eps4 = std::strtof(spec.get("bn_eps_4d").c_str(), nullptr);
+  if (!spec.get("bn_eps_2d").empty()) m->eps2 = std::strtof(spec.get("bn_eps_2d").c_str(), nullptr);
   if (const char* e = std::getenv("VOXEMB_NO_WIN")) m->no_win = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_NO_RR")) m->no_rr = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_RR_WPX")) m->rr_wpx = std::atoi(e);
