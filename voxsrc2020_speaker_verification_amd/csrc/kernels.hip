@@ -701,8 +701,19 @@ __global__ __launch_bounds__(256) void gemm1x1_lds(ConvParams p) {
   const int col = lane & 15, g = lane >> 4;
   const int M = p.N * p.Ho * p.Wo;
   const int HoWo = p.Ho * p.Wo;
-  const int co0 = blockIdx.y * 128;
-  const int px0 = blockIdx.x * 128;
+  // XCD-aware bijective remap (blocks are dealt round-robin over the 8 XCDs):
+  // each XCD gets a contiguous range of logical ids, and within it the cout
+  // blocks of one pixel tile are consecutive, so the activation tile is
+  // fetched into that XCD's L2 once and reused by all cout blocks.
+  const int nwg = gridDim.x;
+  const int cblocks = p.coutp / 128;
+  int lid;
+  {
+    const int bid = blockIdx.x, xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    lid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  const int co0 = (lid % cblocks) * 128;
+  const int px0 = (lid / cblocks) * 128;
   const bf16_t* __restrict__ X = reinterpret_cast<const bf16_t*>(p.x);
   const bf16_t* __restrict__ Wt = reinterpret_cast<const bf16_t*>(p.w);
   // staging assignment: 1024 16-B chunks per operand tile, 4 per thread
@@ -715,30 +726,56 @@ __global__ __launch_bounds__(256) void gemm1x1_lds(ConvParams p) {
     lr[i] = c >> 3;
     lc[i] = c & 7;
     ga[i] = Wt + (size_t)(co0 + lr[i]) * p.kp + lc[i] * 8;
-    const int pix = px0 + lr[i];
-    if (pix < M) {
-      const int n = pix / HoWo, r = pix - (pix / HoWo) * HoWo;
-      const int ho = r / p.Wo, wo = r - (r / p.Wo) * p.Wo;
-      gb[i] = X + (((size_t)n * p.H + ho * p.sh) * p.W + wo * p.sw) * p.ldx + lc[i] * 8;
-    } else {
-      gb[i] = nullptr;
-    }
+    // rows past M load pixel M-1 (any valid address): their output columns
+    // are never stored, and unconditional loads keep the pipeline branch-free
+    const int pix = min(px0 + lr[i], M - 1);
+    const int n = pix / HoWo, r = pix - (pix / HoWo) * HoWo;
+    const int ho = r / p.Wo, wo = r - (r / p.Wo) * p.Wo;
+    gb[i] = X + (((size_t)n * p.H + ho * p.sh) * p.W + wo * p.sw) * p.ldx + lc[i] * 8;
   }
-  uint4 ra[4], rb[4];
-  auto gload = [&](int k0) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      ra[i] = *reinterpret_cast<const uint4*>(ga[i] + k0);
-      rb[i] = gb[i] ? *reinterpret_cast<const uint4*>(gb[i] + k0) : make_uint4(0, 0, 0, 0);
-    }
-  };
-  auto lstore = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      *reinterpret_cast<uint4*>(&As[buf][swz(lr[i], lc[i])]) = ra[i];
-      *reinterpret_cast<uint4*>(&Bs[buf][swz(lr[i], lc[i])]) = rb[i];
-    }
-  };
+  // staging registers as named scalars (arrays captured by a lambda were
+  // promoted to LDS by the compiler).  Two register sets x/y give a 2-deep
+  // prefetch: while tile k is computed from LDS, tile k+1 waits in one set
+  // (loaded an iteration earlier) and tile k+2 is in flight into the other.
+  uint4 xa0, xa1, xa2, xa3, xb0, xb1, xb2, xb3;
+  uint4 ya0, ya1, ya2, ya3, yb0, yb1, yb2, yb3;
+  const int so0 = swz(lr[0], lc[0]), so1 = swz(lr[1], lc[1]), so2 = swz(lr[2], lc[2]),
+            so3 = swz(lr[3], lc[3]);
+#define GEMM_GLOAD(P, k0)                                     \
+  do {                                                        \
+    P##a0 = *reinterpret_cast<const uint4*>(ga[0] + (k0));    \
+    P##a1 = *reinterpret_cast<const uint4*>(ga[1] + (k0));    \
+    P##a2 = *reinterpret_cast<const uint4*>(ga[2] + (k0));    \
+    P##a3 = *reinterpret_cast<const uint4*>(ga[3] + (k0));    \
+    P##b0 = *reinterpret_cast<const uint4*>(gb[0] + (k0));    \
+    P##b1 = *reinterpret_cast<const uint4*>(gb[1] + (k0));    \
+    P##b2 = *reinterpret_cast<const uint4*>(gb[2] + (k0));    \
+    P##b3 = *reinterpret_cast<const uint4*>(gb[3] + (k0));    \
+  } while (0)
+#define GEMM_LSTORE(P, buf)                                   \
+  do {                                                        \
+    *reinterpret_cast<uint4*>(&As[buf][so0]) = P##a0;         \
+    *reinterpret_cast<uint4*>(&As[buf][so1]) = P##a1;         \
+    *reinterpret_cast<uint4*>(&As[buf][so2]) = P##a2;         \
+    *reinterpret_cast<uint4*>(&As[buf][so3]) = P##a3;         \
+    *reinterpret_cast<uint4*>(&Bs[buf][so0]) = P##b0;         \
+    *reinterpret_cast<uint4*>(&Bs[buf][so1]) = P##b1;         \
+    *reinterpret_cast<uint4*>(&Bs[buf][so2]) = P##b2;         \
+    *reinterpret_cast<uint4*>(&Bs[buf][so3]) = P##b3;         \
+  } while (0)
+#define GEMM_COMPUTE(cur)                                                                    \
+  do {                                                                                       \
+    _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) {                                       \
+      const int c = ks * 4 + g;                                                              \
+      bf16x8 a[4], b[4];                                                                     \
+      _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                        \
+        a[i] = *reinterpret_cast<const bf16x8*>(&As[cur][swz(wm * 64 + 16 * i + col, c)]);   \
+        b[i] = *reinterpret_cast<const bf16x8*>(&Bs[cur][swz(wn * 64 + 16 * i + col, c)]);   \
+      }                                                                                      \
+      _Pragma("unroll") for (int i = 0; i < 4; ++i)                                          \
+        _Pragma("unroll") for (int j = 0; j < 4; ++j) acc[i][j] = mfma_step(a[i], b[j], acc[i][j]); \
+    }                                                                                        \
+  } while (0)
   f32x4 acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -746,35 +783,49 @@ __global__ __launch_bounds__(256) void gemm1x1_lds(ConvParams p) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int KT = p.kp / 64;
-  gload(0);
-  lstore(0);
+  const int last = (KT - 1) * 64;
+  // loads past the last tile re-read it: harmless, and keeps the loop
+  // branch-free (a branch lets the compiler fuse the load and store blocks)
+  GEMM_GLOAD(x, 0);
+  GEMM_LSTORE(x, 0);
+  GEMM_GLOAD(x, min(64, last));
   __syncthreads();
-  for (int kt = 0; kt < KT; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < KT) gload((kt + 1) * 64);
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int c = ks * 4 + g;
-      bf16x8 a[4], b[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        a[i] = *reinterpret_cast<const bf16x8*>(&As[cur][swz(wm * 64 + 16 * i + col, c)]);
-        b[i] = *reinterpret_cast<const bf16x8*>(&Bs[cur][swz(wn * 64 + 16 * i + col, c)]);
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mfma_step(a[i], b[j], acc[i][j]);
-    }
-    if (kt + 1 < KT) lstore(cur ^ 1);
+  int kt = 0;
+  for (; kt + 1 < KT; kt += 2) {
+    GEMM_GLOAD(y, min((kt + 2) * 64, last));
+    __builtin_amdgcn_sched_barrier(0);
+    GEMM_COMPUTE(0);
+    __builtin_amdgcn_sched_barrier(0);
+    GEMM_LSTORE(x, 1);
+    __syncthreads();
+    GEMM_GLOAD(x, min((kt + 3) * 64, last));
+    __builtin_amdgcn_sched_barrier(0);
+    GEMM_COMPUTE(1);
+    __builtin_amdgcn_sched_barrier(0);
+    GEMM_LSTORE(y, 0);
     __syncthreads();
   }
+  if (kt < KT) GEMM_COMPUTE(0);  // odd KT: the final tile is in buffer 0
 
+#undef GEMM_GLOAD
+#undef GEMM_LSTORE
+#undef GEMM_COMPUTE
   // paired epilogue: m-tiles (2q, 2q+1) of this wave -> 8 consecutive channels
   const bf16_t* __restrict__ R = reinterpret_cast<const bf16_t*>(p.res);
   bf16_t* __restrict__ Y = reinterpret_cast<bf16_t*>(p.y);
   bf16_t* __restrict__ Y2 = reinterpret_cast<bf16_t*>(p.y2);
   const int flags = p.flags;
+  bf16x8 rvs[2][4];  // residual operands first, off the dependent path
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int ch = co0 + wm * 64 + 32 * q + 8 * g;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int pix = px0 + wn * 64 + 16 * j + col;
+      rvs[q][j] = ((flags & EPI_RES) && ch < p.Cout && ch < p.ysplit && pix < M)
+                      ? ld16(R + (size_t)pix * p.ldr + ch) : bf16x8{};
+    }
+  }
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     const int ch = co0 + wm * 64 + 32 * q + 8 * g;
@@ -807,10 +858,9 @@ __global__ __launch_bounds__(256) void gemm1x1_lds(ConvParams p) {
           v[4 + e] = (v[4 + e] - bm1[e]) * bi1[e];
         }
       }
-      if ((flags & EPI_RES) && ch < p.ysplit) {
-        bf16x8 rv = ld16(R + (size_t)pix * p.ldr + ch);
+      if (flags & EPI_RES) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] += (float)rv[e];
+        for (int e = 0; e < 8; ++e) v[e] += (float)rvs[q][j][e];
       }
       if (flags & EPI_RELU) {
 #pragma unroll
@@ -828,7 +878,7 @@ __global__ __launch_bounds__(256) void gemm1x1_lds(ConvParams p) {
 
 hipError_t launch_gemm1x1(const ConvParams& p, hipStream_t s) {
   const int M = p.N * p.Ho * p.Wo;
-  dim3 grid((M + 127) / 128, p.coutp / 128, 1);
+  dim3 grid(((M + 127) / 128) * (p.coutp / 128), 1, 1);
   hipLaunchKernelGGL(gemm1x1_lds, grid, dim3(256), 0, s, p);
   return hipGetLastError();
 }
