@@ -32,6 +32,8 @@ PEAK_HBM_GBS = 8000.0       # HBM3E spec
 
 def _kernel_name(tag, dt):
     kind = tag & 15
+    if tag & (1 << 22):
+        return f"split_chain<{(tag >> 4) & 15}, {(tag >> 8) & 15}>"
     if tag & (1 << 21):
         return "gemm1x1_lds"
     if tag & (1 << 20):

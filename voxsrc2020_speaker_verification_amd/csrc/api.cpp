@@ -186,6 +186,7 @@ struct Op {
   const void* src = nullptr; void* dst = nullptr; int N = 0, H = 0, W = 0, C = 0, lds = 0, ldd = 0,
              Ho = 0, Wo = 0;
   int64_t count = 0;
+  ChainParams ch{};
   double flops = 0, bytes = 0;
 };
 
@@ -214,6 +215,8 @@ struct vox_model {
   bool no_win = false;         // VOXEMB_NO_WIN=1: disable conv_win (A/B testing)
   bool no_rr = false;          // VOXEMB_NO_RR=1: disable conv1x1_rr
   bool no_gemm = false;        // VOXEMB_NO_GEMM=1: disable gemm1x1_lds
+  bool no_chain = false;       // VOXEMB_NO_CHAIN=1: unfused Res2Net branches
+  int chain_r = 0, chain_wpx = 0, chain_nw = 0;  // VOXEMB_CHAIN_R / VOXEMB_CHAIN_WPX (tuning)
   int rr_wpx = 0, rr_wco = 0;  // VOXEMB_RR_WPX / VOXEMB_RR_WCO: tile overrides (tuning)
 };
 
@@ -503,43 +506,62 @@ static void emit_conv(Builder& B, const ConvW& cw, Act x, const void* x2, int ld
         cw.cout >= 256)
       op.type = 9;
   }
-  // stride-1 bf16 convs without prologue: window-staged LDS kernel if it fits
-  if (op.type == 0 && B.m->dt == BF16 && dt_override != F32 && cw.wtc && sh == 1 && sw == 1 && !in_mean &&
-      Ho == x.H && Wo == x.W && !(flags & EPI_PARTIAL) && !B.m->no_win) {
+  // bf16 convs (stride 1 or 2) without prologue: window-staged LDS kernel if
+  // some (pixel tile, cout tile, channel chunk) fits the LDS budget
+  // stride 2 only pays off for wide inputs (measured: L4 yes, L2/L3 no)
+  if (op.type == 0 && B.m->dt == BF16 && dt_override != F32 && cw.wtc && sh == sw &&
+      (sh == 1 || (sh == 2 && cw.cin >= 192)) && !in_mean && !(flags & EPI_PARTIAL) &&
+      !B.m->no_win) {
     const int taps = cw.kh * cw.kw;
     const int minoff = -(ph * x.W + pw);
     const int maxoff = ((cw.kh - 1) * dh - ph) * x.W + (cw.kw - 1) * dw - pw;
-    const int BCO = 16 * cw.wco;
-    const int kcs[] = {cw.cin, 256, 128, 64, 32};
+    const int HoWo = Ho * Wo;
+    auto in_flat = [&](long pix) -> long {
+      const long n = pix / HoWo, r = pix % HoWo;
+      return (n * x.H + (r / Wo) * sh) * (long)x.W + (r % Wo) * sw;
+    };
+    auto span = [&](int bp) -> long {  // max input-index span of a block's pixels
+      if (sh == 1) return bp - 1;
+      long mx = 0;
+      for (long b0 = 0; b0 < M; b0 += bp)
+        mx = std::max(mx, in_flat(std::min<long>(b0 + bp, M) - 1) - in_flat(b0));
+      return mx;
+    };
+    std::vector<int> wcos = {cw.wco};
+    for (int w : {6, 4, 3, 2, 1})
+      if (w < cw.wco && cw.coutp % (16 * w) == 0) wcos.push_back(w);
+    const int kcs[] = {cw.cin, 256, 128, 64, 32, 16, 8};
+    const int LDS_MAX = 64 * 1024;
     bool done = false;
     for (int wpx : {4, 2, 1}) {
       if (done) break;
       if (wpx > 1 && M < 64 * wpx * 256) continue;  // keep >= 256 blocks when possible
-      for (int kc : kcs) {
-        if (kc > cw.cin || kc % 8) continue;
-        if (kc != cw.cin && kc > 128) continue;
-        int au = kc / 8;
-        if (!(au & 1)) ++au;
-        const int kcp = (taps * kc + 31) / 32 * 32;
-        int wu = kcp / 8;
-        if (!(wu & 1)) ++wu;
-        const int len = 64 * wpx + maxoff - minoff;
-        const int lds = len * au * 16 + BCO * wu * 16 + (kcp / 8) * 16;
-        if (lds > 64 * 1024) continue;
-        p.win_lo = minoff; p.win_len = len; p.win_kc = kc;
-        p.win_astr = au * 16; p.win_wstr = wu * 16; p.win_lds = lds;
-        p.w = cw.wtc->p;
-        op.cl.wpx = wpx;
-        op.type = 7;
-        done = true;
-        break;
+      const long len = span(64 * wpx) + 1 + maxoff - minoff;
+      for (int wco : wcos) {
+        if (done) break;
+        for (int kc : kcs) {
+          if (kc > cw.cin || kc % 8) continue;
+          if (kc != cw.cin && kc > 128) continue;
+          int au = kc / 8;
+          if (!(au & 1)) ++au;
+          const int kcp = (taps * kc + 31) / 32 * 32;
+          int wu = kcp / 8;
+          if (!(wu & 1)) ++wu;
+          const long lds = len * au * 16 + 16L * wco * wu * 16 + (kcp / 8) * 16;
+          if (lds > LDS_MAX) continue;
+          p.win_lo = minoff; p.win_len = (int)len; p.win_kc = kc;
+          p.win_astr = au * 16; p.win_wstr = wu * 16; p.win_lds = (int)lds;
+          p.w = cw.wtc->p;
+          p.cblocks = cw.coutp / (16 * wco);
+          op.cl.wco = wco;
+          op.cl.wpx = wpx;
+          op.type = 7;
+          done = true;
+          break;
+        }
       }
     }
   }
-  const double es = dt_override == F32 ? 4.0 : (double)es_of(B.m);
-  op.flops = 2.0 * M * cw.cout * cw.groups * (double)cw.kh * cw.kw * cw.cin;
-  op.bytes = es * ((double)x.N * x.H * x.W * cw.cin * cw.groups * (x2 ? 2 : 1) +
-                   (double)M * cw.cout * cw.groups * (res ? 2 : 1));
   B.ops->push_back(op);
 }
 
@@ -674,7 +696,56 @@ static int build_res2net(Builder& B, const float* x, int n, int t, float* out) {
       } else {
         emit_conv(B, c1a, cur, nullptr, 0, 1, 1, 1, 1, 0, 0, H, W, A, sw, EPI_AFFINE | EPI_RELU);
       }
-      for (int j = 0; j < s - 1; ++j) {  // res2net_pad_conv_bn_relu :53-75
+      bool chained = false;
+      if (stride == 1 && m->dt == BF16 && !m->no_chain && w % 8 == 0) {
+        // fused split chain: all s-1 branches in one launch (kernels.hip split_chain)
+        const ConvW& b0 = m->convs[ci];
+        ChainParams q{};
+        q.a = A; q.lda = sw; q.b = Bc; q.ldb = sw;
+        q.N = n; q.H = H; q.W = W; q.w = w; q.nst = s - 1; q.coutp = b0.coutp;
+        int au = w / 8;
+        if (!(au & 1)) ++au;
+        q.astr = au * 16;
+        q.kcp = (9 * w + 31) / 32 * 32;
+        int wu = q.kcp / 8;
+        if (!(wu & 1)) ++wu;
+        q.wstr = wu * 16;
+        const long fixed = (long)16 * b0.wco * q.wstr + (q.kcp / 8) * 16;
+        int R = 0;
+        for (int r = 16; r >= 1; --r) {
+          const long buf = (long)(r + 2 * q.nst) * W * q.astr;
+          if (2 * buf + fixed <= 160 * 1024) { R = r; break; }
+        }
+        if (m->chain_r > 0) R = std::min(R, m->chain_r);
+        bool ok = R > 0 && s - 1 <= 8 && b0.wtc && (b0.wco <= 4 || b0.wco == 6);
+        for (int j = 0; ok && j < s - 1; ++j) ok = m->convs[ci + j].wtc != nullptr;
+        if (ok) {
+          q.R = R;
+          q.nwaves = m->chain_nw > 0 ? m->chain_nw : 8;
+          q.buf_bytes = (R + 2 * q.nst) * W * q.astr;
+          q.lds = (int)(2L * q.buf_bytes + fixed);
+          double fl = 0;
+          for (int j = 0; j < s - 1; ++j) {
+            const ConvW& br = m->convs[ci + j];
+            q.wt[j] = br.wtc->p;
+            q.mean[j] = (const float*)br.mean->p;
+            q.inv[j] = (const float*)br.inv->p;
+            fl += 2.0 * n * H * W * 9.0 * w * w;
+          }
+          Op op;
+          op.kind = OP_CONV;
+          op.type = 10;
+          op.ch = q;
+          op.cl.wco = b0.wco;
+          op.cl.wpx = m->chain_wpx > 0 ? m->chain_wpx : 4;
+          op.flops = fl;
+          op.bytes = (double)es * n * H * W * w * (2.0 * (s - 1));
+          B.ops->push_back(op);
+          ci += s - 1;
+          chained = true;
+        }
+      }
+      for (int j = 0; !chained && j < s - 1; ++j) {  // res2net_pad_conv_bn_relu :53-75
         const ConvW& br = m->convs[ci++];
         Act xin{A ? A + (size_t)j * w * es : nullptr, sw, n, H, W, w};
         const void* add = (stride == 1 && j > 0 && Bc) ? Bc + (size_t)(j - 1) * w * es : nullptr;
@@ -826,6 +897,7 @@ static hipError_t run_op(vox_model* m, const Op& op, hipStream_t s) {
     case 7: return launch_conv_win(op.cp, op.cl, s);
     case 8: return launch_conv1x1_rr(op.cp, op.cl, s);
     case 9: return launch_gemm1x1(op.cp, s);
+    case 10: return launch_split_chain(op.ch, op.cl.wco, op.cl.wpx, s);
     case 5: return launch_conv(F32, op.cp, op.cl, s);
     case 1:
       return launch_splitk_reduce(op.part, op.S, op.M, op.coutp, op.cout, op.mean, op.inv,
@@ -881,6 +953,10 @@ extern "C" int vox_load_blob(const void* blob, size_t nbytes, int device, int pr
   if (const char* e = std::getenv("VOXEMB_NO_RR")) m->no_rr = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_RR_WPX")) m->rr_wpx = std::atoi(e);
   if (const char* e = std::getenv("VOXEMB_NO_GEMM")) m->no_gemm = std::atoi(e) != 0;
+  if (const char* e = std::getenv("VOXEMB_NO_CHAIN")) m->no_chain = std::atoi(e) != 0;
+  if (const char* e = std::getenv("VOXEMB_CHAIN_R")) m->chain_r = std::atoi(e);
+  if (const char* e = std::getenv("VOXEMB_CHAIN_WPX")) m->chain_wpx = std::atoi(e);
+  if (const char* e = std::getenv("VOXEMB_CHAIN_NW")) m->chain_nw = std::atoi(e);
   if (const char* e = std::getenv("VOXEMB_RR_WCO")) m->rr_wco = std::atoi(e);
   if ((rc = load_weights(m.get(), ts))) return rc;
   HIPCHK(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking));
@@ -1003,6 +1079,8 @@ extern "C" int vox_profile(vox_model* m, const float* d_x, int n, int t, int f, 
         tag |= (o.cl.wco << 4) | (o.cl.wpx << 8) | (1 << 15);
       else if (o.type == 9)
         tag |= (1 << 21);
+      else if (o.type == 10)
+        tag |= (o.cl.wco << 4) | (o.cl.wpx << 8) | (1 << 22);
       else if (o.type == 8)
         tag |= (o.cl.wco << 4) | (o.cl.wpx << 8) | (((o.cp.cinp + 31) / 32) << 16) | (1 << 20);
       else if (o.type == 0 || o.type == 5)
@@ -1024,7 +1102,7 @@ extern "C" int vox_plan_describe(vox_model* m, const float* d_x, int n, int t, i
   if ((rc = ensure_plan(m, d_x, n, t, (float*)m->stage_out.p))) return rc;
   std::string out;
   static const char* tn[] = {"igemm", "reduce", "pool", "avgpool", "convert", "igemm32", "bnrelu",
-                             "win", "rr", "gemm"};
+                             "win", "rr", "gemm", "chain"};
   for (const Op& o : m->plan) {
     char line[256];
     const ConvParams& p = o.cp;
@@ -1034,6 +1112,10 @@ extern "C" int vox_plan_describe(vox_model* m, const float* d_x, int n, int t, i
                     "g=%d flags=%d x2=%d pro=%d flops=%.4g bytes=%.4g\n",
                     tn[o.type], o.cl.wco, o.cl.wpx, o.cl.splitk, p.N, p.H, p.W, p.Cin, p.Ho, p.Wo,
                     p.Cout, p.kh, p.kw, p.sh, p.groups, p.flags, p.x2 ? 1 : 0, p.in_mean ? 1 : 0,
+                    o.flops, o.bytes);
+    else if (o.type == 10)
+      std::snprintf(line, sizeof(line), "chain wco=%d wpx=%d N=%d H=%d W=%d w=%d nst=%d R=%d lds=%d flops=%.4g bytes=%.4g\n",
+                    o.cl.wco, o.cl.wpx, o.ch.N, o.ch.H, o.ch.W, o.ch.w, o.ch.nst, o.ch.R, o.ch.lds,
                     o.flops, o.bytes);
     else
       std::snprintf(line, sizeof(line), "%s N=%d H=%d W=%d C=%d bytes=%.4g\n", tn[o.type], o.N,

@@ -46,6 +46,21 @@ struct ConvLaunch {
 
 // Returns hipSuccess or the launch error.
 hipError_t launch_conv(DType t, const ConvParams& p, const ConvLaunch& l, hipStream_t s);
+// Fused Res2Net split-scale chain (stride 1, res2net_model.py:53-75):
+//   y_0 = relu(bn_0(conv_0(x_0))), y_k = relu(bn_k(conv_k(x_k + y_{k-1})))
+// for k < nst = split-1, x_k = a[:, k*w:(k+1)*w], y_k -> b[:, k*w:(k+1)*w].
+struct ChainParams {
+  const void* a; int lda;
+  void* b; int ldb;
+  const void* wt[8];                // per stage [coutp][9*w] bf16
+  const float* mean[8];
+  const float* inv[8];
+  int N, H, W, w, nst, R, coutp;
+  int astr, wstr, kcp, buf_bytes, lds;
+  int nwaves;                       // 4 or 8 waves per block
+};
+hipError_t launch_split_chain(const ChainParams& q, int wco, int wpx, hipStream_t s);
+
 // Stride-1 bf16 conv with the input window staged in LDS (weights in the
 // [coutp][taps*Cin] layout).
 hipError_t launch_conv_win(const ConvParams& p, const ConvLaunch& l, hipStream_t s);

@@ -329,11 +329,12 @@ __global__ __launch_bounds__(256) void conv_win(ConvParams p) {
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int col = lane & 15;
-  const int M = p.N * p.H * p.W;
+  const int M = p.N * p.Ho * p.Wo;           // output pixels
+  const int Min = p.N * p.H * p.W;           // input pixels
+  const int HoWo = p.Ho * p.Wo;
   const int p0 = blockIdx.x * (64 * WPX);
   const int co0 = blockIdx.y * BCO;
   const int taps = p.kh * p.kw;
-  const int HW = p.H * p.W;
   char* act = smem;
   char* wts = smem + p.win_len * p.win_astr;
   int4* ktab = reinterpret_cast<int4*>(wts + BCO * p.win_wstr);
@@ -341,6 +342,14 @@ __global__ __launch_bounds__(256) void conv_win(ConvParams p) {
   const bf16_t* __restrict__ X2 = reinterpret_cast<const bf16_t*>(p.x2);
   const bf16_t* __restrict__ Wt = reinterpret_cast<const bf16_t*>(p.w);
   const int pbase = p0 + wave * 16 * WPX;
+  // window in input-flattened coordinates: tap (dy,dx) of the output pixel
+  // whose centre input pixel is c sits at c + dy*W + dx (stride 1 or 2)
+  auto in_flat = [&](int pix) {
+    const int n = pix / HoWo, r = pix - (pix / HoWo) * HoWo;
+    const int ho = r / p.Wo, wo = r - (r / p.Wo) * p.Wo;
+    return (n * p.H + ho * p.sh) * p.W + wo * p.sw;
+  };
+  const int wstart = in_flat(min(p0, M - 1)) + p.win_lo;
 
   int hh[WPX], ww[WPX], li[WPX];
   bool pv[WPX];
@@ -349,10 +358,11 @@ __global__ __launch_bounds__(256) void conv_win(ConvParams p) {
     const int pix = pbase + 16 * j + col;
     pv[j] = pix < M;
     const int q = pv[j] ? pix : 0;
-    const int r = q % HW;
-    hh[j] = r / p.W;
-    ww[j] = r - hh[j] * p.W;
-    li[j] = pix - p0 - p.win_lo;
+    const int r = q % HoWo;
+    const int ho = r / p.Wo, wo = r - (r / p.Wo) * p.Wo;
+    hh[j] = ho * p.sh;
+    ww[j] = wo * p.sw;
+    li[j] = in_flat(q) - wstart;
   }
   f32x4 acc[WCO][WPX];
 #pragma unroll
@@ -396,7 +406,7 @@ __global__ __launch_bounds__(256) void conv_win(ConvParams p) {
     {
       const int cu = kc >> 3;
       const int total = p.win_len * cu;
-      const int gbase = p0 + p.win_lo;
+      const int gbase = wstart;
       for (int b0 = tid; b0 < total; b0 += 4 * 256) {
         uint4 v[4];
 #pragma unroll
@@ -406,7 +416,7 @@ __global__ __launch_bounds__(256) void conv_win(ConvParams p) {
           if (idx < total) {
             const int wp = idx / cu, u = idx - (idx / cu) * cu;
             const int gp = gbase + wp;
-            if (gp >= 0 && gp < M) {
+            if (gp >= 0 && gp < Min) {
               v[r] = *reinterpret_cast<const uint4*>(X + (size_t)gp * p.ldx + c0 + u * 8);
               if (X2) {
                 bf16x8 a = __builtin_bit_cast(bf16x8, v[r]);
@@ -453,7 +463,7 @@ __global__ __launch_bounds__(256) void conv_win(ConvParams p) {
 
 template <int WCO, int WPX>
 static hipError_t launch_win_t(const ConvParams& p, hipStream_t s) {
-  const int M = p.N * p.H * p.W;
+  const int M = p.N * p.Ho * p.Wo;
   dim3 grid((M + 64 * WPX - 1) / (64 * WPX), p.cblocks, 1);
   hipLaunchKernelGGL((conv_win<WCO, WPX>), grid, dim3(256), p.win_lds, s, p);
   return hipGetLastError();
@@ -881,6 +891,208 @@ hipError_t launch_gemm1x1(const ConvParams& p, hipStream_t s) {
   dim3 grid(((M + 127) / 128) * (p.coutp / 128), 1, 1);
   hipLaunchKernelGGL(gemm1x1_lds, grid, dim3(256), 0, s, p);
   return hipGetLastError();
+}
+
+// ----------------------------------------------------------------------------
+// Fused hierarchical split-scale chain (Res2Net, stride 1).  A block owns R
+// full-width output rows of one utterance and runs all nst = split-1 branch
+// convolutions on them, keeping every intermediate in LDS:
+//   buffer rows map to image rows r0-nst .. r0+R+nst (zeros outside the image);
+//   stage k reads rows [r0-(nst-k), r0+R+(nst-k)) and produces rows
+//   [r0-(nst-1-k), r0+R+(nst-1-k)) -- the halo shrinks by one row per stage;
+//   before stage k the next input x_{k+1} is staged into the other buffer and
+//   stage k's epilogue adds y_k into it (z_{k+1} = x_{k+1} + y_k, rounded to
+//   bf16 like the unfused path); y_k for the R central rows goes to HBM.
+// Only x_0..x_{nst-1} are read and y_0..y_{nst-1} written: the intermediate
+// branch tensors and the hierarchical adds never touch HBM.
+template <int WCO, int WPX, int NW>
+__global__ __launch_bounds__(64 * NW) void split_chain(ChainParams q) {
+  constexpr int NT = 64 * NW;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int BCO = 16 * WCO;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int col = lane & 15, g = lane >> 4;
+  const int W = q.W, H = q.H, w = q.w, nst = q.nst, R = q.R;
+  const int tiles_img = (H + R - 1) / R;
+  const int n = blockIdx.x / tiles_img;
+  const int r0 = (blockIdx.x - n * tiles_img) * R;
+  const int rbase = r0 - nst;                       // image row of buffer row 0
+  char* buf0 = smem;
+  char* buf1 = smem + q.buf_bytes;
+  char* wts = smem + 2 * q.buf_bytes;
+  int4* ktab = reinterpret_cast<int4*>(wts + BCO * q.wstr);
+  const bf16_t* __restrict__ A = reinterpret_cast<const bf16_t*>(q.a);
+  bf16_t* __restrict__ Bo = reinterpret_cast<bf16_t*>(q.b);
+  const size_t img = (size_t)n * H * W;
+  const int kflat = 9 * w;
+  const int units = q.kcp >> 3;
+  for (int u = tid; u < units; u += NT) {
+    const int k = u * 8;
+    int4 e = make_int4(0, 0, 1 << 20, 1 << 20);
+    if (k < kflat) {
+      const int tap = k / w, ch = k - (k / w) * w;
+      const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+      e = make_int4(dy * W + dx, ch * 2, dy, dx);
+    }
+    ktab[u] = e;
+  }
+  // copy channels [c0, c0+w) of image rows [ra, rb) into an LDS buffer.
+  // Thread t owns 16-B chunk t of every row (pixel t/cu, chunk t%cu, computed
+  // once); rows are unrolled 8-deep so each thread keeps 8 loads in flight.
+  const int cu = w >> 3;
+  const int rowchunks = W * cu;
+  const int my_px = tid / cu, my_u = tid - (tid / cu) * cu;
+  auto stage_rows = [&](char* dst, int c0, int ra, int rb) __attribute__((always_inline)) {
+    for (int cbase = 0; cbase < rowchunks; cbase += NT) {
+      const int c = cbase + tid;
+      if (c >= rowchunks) break;
+      const int px = (cbase == 0) ? my_px : c / cu;
+      const int uu = (cbase == 0) ? my_u : c - (c / cu) * cu;
+      const bf16_t* src = A + (img + px) * q.lda + c0 + uu * 8;
+      char* d = dst + px * q.astr + uu * 16;
+      for (int row = ra; row < rb; row += 8) {
+        uint4 v[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const int rr = row + r;
+          v[r] = (rr < rb && rr >= 0 && rr < H)
+                     ? *reinterpret_cast<const uint4*>(src + (size_t)rr * W * q.lda)
+                     : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+          if (row + r < rb)
+            *reinterpret_cast<uint4*>(d + (row + r - rbase) * W * q.astr) = v[r];
+      }
+    }
+  };
+  stage_rows(buf0, 0, r0 - nst, r0 + R + nst);
+
+  for (int k = 0; k < nst; ++k) {
+    // stage-k weights [BCO][kcp] (rows >= w are zero in the global layout)
+    {
+      const bf16_t* __restrict__ Wt = reinterpret_cast<const bf16_t*>(q.wt[k]);
+      const int total = BCO * units;
+      for (int b0 = tid; b0 < total; b0 += 8 * NT) {
+        uint4 v[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const int idx = b0 + r * NT;
+          const int rw = idx / units, u = idx - (idx / units) * units;
+          v[r] = (idx < total && u * 8 < kflat)
+                     ? *reinterpret_cast<const uint4*>(Wt + (size_t)rw * kflat + u * 8)
+                     : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const int idx = b0 + r * NT;
+          if (idx < total) {
+            const int rw = idx / units, u = idx - (idx / units) * units;
+            *reinterpret_cast<uint4*>(wts + rw * q.wstr + u * 16) = v[r];
+          }
+        }
+      }
+    }
+    const int ext = nst - 1 - k;
+    const int oa = r0 - ext, ob = r0 + R + ext;     // output image rows of this stage
+    char* in = (k & 1) ? buf1 : buf0;
+    char* out = (k & 1) ? buf0 : buf1;
+    if (k + 1 < nst) stage_rows(out, (k + 1) * w, oa, ob);
+    __syncthreads();
+    const float* __restrict__ bm = q.mean[k];
+    const float* __restrict__ bi = q.inv[k];
+    const int npix = (ob - oa) * W;
+    const int ntiles = (npix + 15) >> 4;
+    for (int t0 = wave * WPX; t0 < ntiles; t0 += NW * WPX) {
+      int prow[WPX], pcol[WPX];
+      bool pv[WPX];
+#pragma unroll
+      for (int j = 0; j < WPX; ++j) {
+        const int lp = (t0 + j) * 16 + col;
+        pv[j] = lp < npix;
+        const int l = pv[j] ? lp : 0;
+        prow[j] = oa + l / W;
+        pcol[j] = l - (l / W) * W;
+        pv[j] = pv[j] && prow[j] >= 0 && prow[j] < H;
+      }
+      f32x4 acc[WCO][WPX];
+#pragma unroll
+      for (int i = 0; i < WCO; ++i)
+#pragma unroll
+        for (int j = 0; j < WPX; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int k0 = 0; k0 < q.kcp; k0 += 32) {
+        const int4 e = ktab[(k0 >> 3) + g];
+        bf16x8 a[WCO], b[WPX];
+#pragma unroll
+        for (int i = 0; i < WCO; ++i)
+          a[i] = *reinterpret_cast<const bf16x8*>(wts + (16 * i + col) * q.wstr + (k0 + 8 * g) * 2);
+#pragma unroll
+        for (int j = 0; j < WPX; ++j) {
+          const int yy = prow[j] + e.z, xx = pcol[j] + e.w;
+          const bool ok = pv[j] && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
+          b[j] = ok ? *reinterpret_cast<const bf16x8*>(
+                          in + ((prow[j] - rbase) * W + pcol[j] + e.x) * q.astr + e.y)
+                    : bf16x8{};
+        }
+#pragma unroll
+        for (int i = 0; i < WCO; ++i)
+#pragma unroll
+          for (int j = 0; j < WPX; ++j) acc[i][j] = mfma_step(a[i], b[j], acc[i][j]);
+      }
+      // epilogue: y = relu(bn(acc)) -> HBM (central rows) and z_{k+1} += y in LDS
+#pragma unroll
+      for (int i = 0; i < WCO; ++i) {
+        const int co = 16 * i + 4 * g;
+        if (co >= w) continue;
+        const f32x4 m = *reinterpret_cast<const f32x4*>(bm + co);
+        const f32x4 sc = *reinterpret_cast<const f32x4*>(bi + co);
+#pragma unroll
+        for (int j = 0; j < WPX; ++j) {
+          if (!pv[j]) continue;
+          bf16x4 y;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) y[r] = (bf16_t)fmaxf((acc[i][j][r] - m[r]) * sc[r], 0.f);
+          if (prow[j] >= r0 && prow[j] < r0 + R)
+            *reinterpret_cast<bf16x4*>(Bo + (img + (size_t)prow[j] * W + pcol[j]) * q.ldb + k * w + co) = y;
+          if (k + 1 < nst) {
+            bf16x4* zp = reinterpret_cast<bf16x4*>(out + ((prow[j] - rbase) * W + pcol[j]) * q.astr + co * 2);
+            bf16x4 x = *zp, z;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) z[r] = (bf16_t)((float)x[r] + (float)y[r]);
+            *zp = z;
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+template <int WCO, int WPX>
+static hipError_t launch_chain_t(const ChainParams& q, hipStream_t s) {
+  const int blocks = q.N * ((q.H + q.R - 1) / q.R);
+  if (q.nwaves == 8)
+    hipLaunchKernelGGL((split_chain<WCO, WPX, 8>), dim3(blocks), dim3(512), q.lds, s, q);
+  else
+    hipLaunchKernelGGL((split_chain<WCO, WPX, 4>), dim3(blocks), dim3(256), q.lds, s, q);
+  return hipGetLastError();
+}
+
+hipError_t launch_split_chain(const ChainParams& q, int wco, int wpx, hipStream_t s) {
+#define CH_CASE(C)                                                        \
+  case C:                                                                 \
+    return wpx == 4 ? launch_chain_t<C, 4>(q, s)                          \
+                    : (wpx == 2 ? launch_chain_t<C, 2>(q, s) : launch_chain_t<C, 1>(q, s));
+  switch (wco) {
+    CH_CASE(1)
+    CH_CASE(2)
+    CH_CASE(3)
+    CH_CASE(4)
+    CH_CASE(6)
+  }
+#undef CH_CASE
+  return hipErrorInvalidValue;
 }
 
 int conv_kstep(DType t) { return t == BF16 ? Tr<bf16_t>::KSTEP : Tr<float>::KSTEP; }
