@@ -32,6 +32,8 @@ PEAK_HBM_GBS = 8000.0       # HBM3E spec
 
 def _kernel_name(tag, dt):
     kind = tag & 15
+    if tag & (1 << 23):
+        return "stem_conv1"
     if tag & (1 << 22):
         return f"split_chain<{(tag >> 4) & 15}, {(tag >> 8) & 15}>"
     if tag & (1 << 21):
@@ -173,7 +175,8 @@ def main():
         g["flops"] += float(fl)
         g["bytes"] += float(by)
         g["n"] += 1
-    conv = {k: v for k, v in groups.items() if k.startswith("conv_")}
+    # the conv stack: every backbone kernel with MFMA work (not the fp32 head)
+    conv = {k: v for k, v in groups.items() if v["flops"] > 0 and v["kind"] == 0}
     dom_name, dom = max(conv.items(), key=lambda kv: kv[1]["ms"])
     peak = PEAK_F32_TFLOPS if "float" in dom_name else PEAK_BF16_TFLOPS
     ach = (dom["flops"] / dom["n"]) / (dom["ms"] / dom["n"] * 1e-3) / 1e12

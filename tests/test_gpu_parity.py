@@ -175,3 +175,20 @@ def test_extract_cli_end_to_end(weights, tmp_path):
         ref = models_ref.embed_utterance(spec, t, kaldi_ref.sliding_cmn(m))
         assert np.abs(got[k] - ref).max() <= 1e-3 * np.abs(ref).max(), k
     assert len(open(tmp_path / "xv.scp").read().splitlines()) == len(mats)
+
+
+@pytest.mark.parametrize("name,F,T", [("res2net50_w24_s4_c32", 80, 200), ("res2net50_w24_s4_c32", 80, 37),
+                                      ("res2net50_w8_s6_c16", 40, 64)])
+def test_fused_kernels_bitwise_equal_unfused(weights, name, F, T, monkeypatch):
+    """The fused split chain and the specialised 1x1/window kernels compute the
+    same bf16 arithmetic as the generic path: embeddings must be identical
+    (VOXEMB_NO_* are read at model load)."""
+    from voxsrc2020_speaker_verification_amd import synth
+    spec, t, blob = weights(name, F)
+    x = synth.make_features(3, T, F, seed=21)
+    with _extractor(blob, "bf16") as ex:
+        fused = ex.run(x)
+    monkeypatch.setenv("VOXEMB_NO_CHAIN", "1")
+    with _extractor(blob, "bf16") as ex:
+        unfused = ex.run(x)
+    assert np.array_equal(fused, unfused)

@@ -156,6 +156,7 @@ struct ConvW {
   std::shared_ptr<DevBuf> w;         // [groups][coutp][kp] in the model dtype
   std::shared_ptr<DevBuf> wtc;       // bf16 [coutp][taps*cin] for conv_win (groups == 1)
   std::shared_ptr<DevBuf> wpair;     // bf16 [coutp][kp] paired-row layout for conv1x1_rr
+  std::shared_ptr<DevBuf> wstem;     // fp32 [9][cout] for the 1-channel 3x3 stem kernel
   std::shared_ptr<DevBuf> mean, inv; // optional epilogue BN (cout*groups)
 };
 
@@ -213,9 +214,11 @@ struct vox_model {
   DevBuf stage_in, stage_out;  // host-API staging
   float eps4 = 1.001e-5f, eps2 = 1e-5f;  // BN epsilons (blob header may override)
   bool no_win = false;         // VOXEMB_NO_WIN=1: disable conv_win (A/B testing)
+  int win_cin = 0;             // VOXEMB_WIN_CIN=c: conv_win only for Cin == c (debug)
   bool no_rr = false;          // VOXEMB_NO_RR=1: disable conv1x1_rr
   bool no_gemm = false;        // VOXEMB_NO_GEMM=1: disable gemm1x1_lds
   bool no_chain = false;       // VOXEMB_NO_CHAIN=1: unfused Res2Net branches
+  bool no_stem = false;        // VOXEMB_NO_STEM=1: stem through the generic conv
   int chain_r = 0, chain_wpx = 0, chain_nw = 0;  // VOXEMB_CHAIN_R / VOXEMB_CHAIN_WPX (tuning)
   int rr_wpx = 0, rr_wco = 0;  // VOXEMB_RR_WPX / VOXEMB_RR_WCO: tile overrides (tuning)
 };
@@ -278,6 +281,21 @@ static int make_conv(vox_model* m, const HostTensor& k, int groups, const HostTe
     out.wpair = std::make_shared<DevBuf>();
     HIPCHK(out.wpair->ensure(h.size() * 2));
     HIPCHK(hipMemcpy(out.wpair->p, h.data(), h.size() * 2, hipMemcpyHostToDevice));
+  }
+  if (groups == 1 && cin == 1 && kh == 3 && kw == 3 && cout <= 64) {
+    std::vector<float> h(9 * (size_t)cout);
+    for (int t = 0; t < 9; ++t)
+      for (int co = 0; co < cout; ++co) {
+        float v = k.data[(size_t)t * cout_all + col0 + co];
+        if (dt == BF16) {  // the same bf16 value the MFMA path would use
+          const uint32_t u = (uint32_t)f2bf(v) << 16;
+          std::memcpy(&v, &u, 4);
+        }
+        h[(size_t)t * cout + co] = v;
+      }
+    out.wstem = std::make_shared<DevBuf>();
+    HIPCHK(out.wstem->ensure(h.size() * 4));
+    HIPCHK(hipMemcpy(out.wstem->p, h.data(), h.size() * 4, hipMemcpyHostToDevice));
   }
   if (dt == BF16 && groups == 1 && cin % 8 == 0) {
     std::vector<uint16_t> h((size_t)out.coutp * taps * cin, 0);
@@ -511,7 +529,7 @@ static void emit_conv(Builder& B, const ConvW& cw, Act x, const void* x2, int ld
   // stride 2 only pays off for wide inputs (measured: L4 yes, L2/L3 no)
   if (op.type == 0 && B.m->dt == BF16 && dt_override != F32 && cw.wtc && sh == sw &&
       (sh == 1 || (sh == 2 && cw.cin >= 192)) && !in_mean && !(flags & EPI_PARTIAL) &&
-      !B.m->no_win) {
+      !B.m->no_win && (!B.m->win_cin || B.m->win_cin == cw.cin)) {
     const int taps = cw.kh * cw.kw;
     const int minoff = -(ph * x.W + pw);
     const int maxoff = ((cw.kh - 1) * dh - ph) * x.W + (cw.kw - 1) * dw - pw;
@@ -537,9 +555,14 @@ static void emit_conv(Builder& B, const ConvW& cw, Act x, const void* x2, int ld
       if (done) break;
       if (wpx > 1 && M < 64 * wpx * 256) continue;  // keep >= 256 blocks when possible
       const long len = span(64 * wpx) + 1 + maxoff - minoff;
+      // pass 0: full K at any cout tile (same tap-major K order as every
+      // other conv path, so results are bitwise identical); pass 1: channel
+      // chunks, largest cout tile first
+      for (int pass = 0; pass < 2 && !done; ++pass)
       for (int wco : wcos) {
         if (done) break;
         for (int kc : kcs) {
+          if (pass == 0 && kc != cw.cin) continue;
           if (kc > cw.cin || kc % 8) continue;
           if (kc != cw.cin && kc > 128) continue;
           int au = kc / 8;
@@ -562,6 +585,10 @@ static void emit_conv(Builder& B, const ConvW& cw, Act x, const void* x2, int ld
       }
     }
   }
+  const double es = dt_override == F32 ? 4.0 : (double)es_of(B.m);
+  op.flops = 2.0 * M * cw.cout * cw.groups * (double)cw.kh * cw.kw * cw.cin;
+  op.bytes = es * ((double)x.N * x.H * x.W * cw.cin * cw.groups * (x2 ? 2 : 1) +
+                   (double)M * cw.cout * cw.groups * (res ? 2 : 1));
   B.ops->push_back(op);
 }
 
@@ -631,6 +658,25 @@ static const void* emit_input(Builder& B, const float* x, int64_t count) {
   return in;
 }
 
+// 1-channel 3x3 stem + BN + ReLU straight from the fp32 features (no cast op)
+static void emit_stem(Builder& B, const ConvW& stem, const float* x, int n, int H, int W, void* y) {
+  if (stem.wstem && !B.m->no_stem) {
+    Op op;
+    op.kind = OP_CONV;
+    op.type = 11;
+    op.src = x; op.dst = y; op.N = n; op.H = H; op.W = W; op.C = stem.cout;
+    op.part = (const float*)stem.wstem->p;
+    op.mean = (const float*)stem.mean->p;
+    op.inv = (const float*)stem.inv->p;
+    op.flops = 2.0 * n * H * W * 9.0 * stem.cout;
+    op.bytes = 4.0 * n * H * W + (double)es_of(B.m) * n * H * W * stem.cout;
+    B.ops->push_back(op);
+    return;
+  }
+  Act in{emit_input(B, x, (int64_t)n * H * W), 1, n, H, W, 1};
+  emit_conv(B, stem, in, nullptr, 0, 1, 1, 1, 1, 1, 1, H, W, y, stem.cout, EPI_AFFINE | EPI_RELU);
+}
+
 static int build_tdnn(Builder& B, const float* x, int n, int t, float* out) {
   vox_model* m = B.m;
   const int F = m->feat_dim;
@@ -662,13 +708,11 @@ static int build_res2net(Builder& B, const float* x, int n, int t, float* out) {
   auto strides = m->spec.getv("block_strides");
   auto widths = m->spec.getv("widths");
   int H = t, W = m->feat_dim;
-  Act in{emit_input(B, x, (int64_t)n * t * W), 1, n, H, W, 1};
   size_t ci = 0;
   const ConvW& stem = m->convs[ci++];
   Slot cur_s = S_X0, nxt_s = S_X1;
   void* y = B.base(cur_s, (size_t)n * H * W * stem.cout * es);
-  emit_conv(B, stem, in, nullptr, 0, 1, 1, 1, 1, 1, 1, H, W, y, stem.cout,
-            EPI_AFFINE | EPI_RELU);  // res2net_model.py:192-203, SAME pad 1
+  emit_stem(B, stem, x, n, H, W, y);  // res2net_model.py:192-203, SAME pad 1
   Act cur{y, stem.cout, n, H, W, stem.cout};
   for (size_t st = 0; st < blocks.size(); ++st) {
     const int w = widths[st];
@@ -710,19 +754,24 @@ static int build_res2net(Builder& B, const float* x, int n, int t, float* out) {
         int wu = q.kcp / 8;
         if (!(wu & 1)) ++wu;
         q.wstr = wu * 16;
-        const long fixed = (long)16 * b0.wco * q.wstr + (q.kcp / 8) * 16;
+        const long fixed = (long)16 * b0.wco * q.wstr + (q.kcp / 8) * 4;
         int R = 0;
+        const int nthreads = 64 * (m->chain_nw > 0 ? m->chain_nw : 8);
         for (int r = 16; r >= 1; --r) {
-          const long buf = (long)(r + 2 * q.nst) * W * q.astr;
-          if (2 * buf + fixed <= 160 * 1024) { R = r; break; }
+          const long buf = (long)(r + 2 * q.nst) * (W + 2) * q.astr;
+          // the next input x_{k+1} (r + 2*(nst-1) rows) is prefetched into 8 chunks/thread
+          const long xchunks = (long)(r + 2 * (q.nst - 1)) * W * (w / 8);
+          if (2 * buf + fixed <= 160 * 1024 && xchunks <= 8L * nthreads) { R = r; break; }
         }
         if (m->chain_r > 0) R = std::min(R, m->chain_r);
-        bool ok = R > 0 && s - 1 <= 8 && b0.wtc && (b0.wco <= 4 || b0.wco == 6);
+        // register-prefetched weights: the kernel holds enough chunks for w <= 16*wco;
+        // keep the widest tile counts (wco 6) out (too many registers)
+        bool ok = R > 0 && s - 1 <= 8 && b0.wtc && b0.wco <= 4 && w <= 16 * b0.wco;
         for (int j = 0; ok && j < s - 1; ++j) ok = m->convs[ci + j].wtc != nullptr;
         if (ok) {
           q.R = R;
           q.nwaves = m->chain_nw > 0 ? m->chain_nw : 8;
-          q.buf_bytes = (R + 2 * q.nst) * W * q.astr;
+          q.buf_bytes = (R + 2 * q.nst) * (W + 2) * q.astr;
           q.lds = (int)(2L * q.buf_bytes + fixed);
           double fl = 0;
           for (int j = 0; j < s - 1; ++j) {
@@ -737,7 +786,7 @@ static int build_res2net(Builder& B, const float* x, int n, int t, float* out) {
           op.type = 10;
           op.ch = q;
           op.cl.wco = b0.wco;
-          op.cl.wpx = m->chain_wpx > 0 ? m->chain_wpx : 4;
+          op.cl.wpx = m->chain_wpx > 0 ? m->chain_wpx : (b0.wco <= 2 ? 4 : 2);  // wco 3 spills at 4
           op.flops = fl;
           op.bytes = (double)es * n * H * W * w * (2.0 * (s - 1));
           B.ops->push_back(op);
@@ -795,13 +844,11 @@ static int build_dpn(Builder& B, const float* x, int n, int t, float* out) {
   auto ksec = m->spec.getv("k_sec");
   auto inc_sec = m->spec.getv("inc_sec");
   int H = t, W = m->feat_dim;
-  Act in{emit_input(B, x, (int64_t)n * t * W), 1, n, H, W, 1};
   size_t ci = 0, bi = 0;
   const ConvW& stem = m->convs[ci++];
   Slot stage_s[2] = {S_X0, S_X1};
   void* y = B.base(S_SC, (size_t)n * H * W * stem.cout * es);
-  emit_conv(B, stem, in, nullptr, 0, 1, 1, 1, 1, 1, 1, H, W, y, stem.cout,
-            EPI_AFFINE | EPI_RELU);  // conv_bn_relu, SAME
+  emit_stem(B, stem, x, n, H, W, y);  // conv_bn_relu, SAME
   Act cur{y, stem.cout, n, H, W, stem.cout};
   for (size_t st = 0; st < ksec.size(); ++st) {
     const int bw = bw0 << st;
@@ -898,6 +945,9 @@ static hipError_t run_op(vox_model* m, const Op& op, hipStream_t s) {
     case 8: return launch_conv1x1_rr(op.cp, op.cl, s);
     case 9: return launch_gemm1x1(op.cp, s);
     case 10: return launch_split_chain(op.ch, op.cl.wco, op.cl.wpx, s);
+    case 11:
+      return launch_stem(m->dt, (const float*)op.src, op.N, op.H, op.W, op.part, op.C, op.mean,
+                         op.inv, op.dst, s);
     case 5: return launch_conv(F32, op.cp, op.cl, s);
     case 1:
       return launch_splitk_reduce(op.part, op.S, op.M, op.coutp, op.cout, op.mean, op.inv,
@@ -950,10 +1000,12 @@ extern "C" int vox_load_blob(const void* blob, size_t nbytes, int device, int pr
   if (!spec.get("bn_eps_4d").empty()) m->eps4 = std::strtof(spec.get("bn_eps_4d").c_str(), nullptr);
   if (!spec.get("bn_eps_2d").empty()) m->eps2 = std::strtof(spec.get("bn_eps_2d").c_str(), nullptr);
   if (const char* e = std::getenv("VOXEMB_NO_WIN")) m->no_win = std::atoi(e) != 0;
+  if (const char* e = std::getenv("VOXEMB_WIN_CIN")) m->win_cin = std::atoi(e);
   if (const char* e = std::getenv("VOXEMB_NO_RR")) m->no_rr = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_RR_WPX")) m->rr_wpx = std::atoi(e);
   if (const char* e = std::getenv("VOXEMB_NO_GEMM")) m->no_gemm = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_NO_CHAIN")) m->no_chain = std::atoi(e) != 0;
+  if (const char* e = std::getenv("VOXEMB_NO_STEM")) m->no_stem = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_CHAIN_R")) m->chain_r = std::atoi(e);
   if (const char* e = std::getenv("VOXEMB_CHAIN_WPX")) m->chain_wpx = std::atoi(e);
   if (const char* e = std::getenv("VOXEMB_CHAIN_NW")) m->chain_nw = std::atoi(e);
@@ -1081,6 +1133,8 @@ extern "C" int vox_profile(vox_model* m, const float* d_x, int n, int t, int f, 
         tag |= (1 << 21);
       else if (o.type == 10)
         tag |= (o.cl.wco << 4) | (o.cl.wpx << 8) | (1 << 22);
+      else if (o.type == 11)
+        tag |= (1 << 23);
       else if (o.type == 8)
         tag |= (o.cl.wco << 4) | (o.cl.wpx << 8) | (((o.cp.cinp + 31) / 32) << 16) | (1 << 20);
       else if (o.type == 0 || o.type == 5)
@@ -1102,7 +1156,7 @@ extern "C" int vox_plan_describe(vox_model* m, const float* d_x, int n, int t, i
   if ((rc = ensure_plan(m, d_x, n, t, (float*)m->stage_out.p))) return rc;
   std::string out;
   static const char* tn[] = {"igemm", "reduce", "pool", "avgpool", "convert", "igemm32", "bnrelu",
-                             "win", "rr", "gemm", "chain"};
+                             "win", "rr", "gemm", "chain", "stem"};
   for (const Op& o : m->plan) {
     char line[256];
     const ConvParams& p = o.cp;

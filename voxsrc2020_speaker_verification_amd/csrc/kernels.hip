@@ -908,49 +908,66 @@ hipError_t launch_gemm1x1(const ConvParams& p, hipStream_t s) {
 template <int WCO, int WPX, int NW>
 __global__ __launch_bounds__(64 * NW) void split_chain(ChainParams q) {
   constexpr int NT = 64 * NW;
+  constexpr int XREG = 8;                 // prefetched x chunks per thread (host-checked)
+  // weight chunks per thread, sized for the widest branch this tile count
+  // serves (w <= 16*WCO): BCO rows x roundup(9*w, 32)/8 16-byte units
+  constexpr int WREG = (16 * WCO * (((9 * 16 * WCO + 31) / 32) * 4) + NT - 1) / NT;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int BCO = 16 * WCO;
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int col = lane & 15, g = lane >> 4;
   const int W = q.W, H = q.H, w = q.w, nst = q.nst, R = q.R;
+  const int WP = W + 2;                             // LDS row: zero column | W | zero column
+  const int rowb = WP * q.astr;                     // bytes per LDS row
   const int tiles_img = (H + R - 1) / R;
   const int n = blockIdx.x / tiles_img;
   const int r0 = (blockIdx.x - n * tiles_img) * R;
   const int rbase = r0 - nst;                       // image row of buffer row 0
+  const int nrows = R + 2 * nst;
   char* buf0 = smem;
   char* buf1 = smem + q.buf_bytes;
   char* wts = smem + 2 * q.buf_bytes;
-  int4* ktab = reinterpret_cast<int4*>(wts + BCO * q.wstr);
+  int* ktab = reinterpret_cast<int*>(wts + BCO * q.wstr);
   const bf16_t* __restrict__ A = reinterpret_cast<const bf16_t*>(q.a);
   bf16_t* __restrict__ Bo = reinterpret_cast<bf16_t*>(q.b);
   const size_t img = (size_t)n * H * W;
   const int kflat = 9 * w;
   const int units = q.kcp >> 3;
+  // k-step table: byte offset of chunk u's tap/channel relative to the
+  // centre pixel (padded K points at a zero pad column of row 0 .. harmless:
+  // the matching weights are zero)
   for (int u = tid; u < units; u += NT) {
     const int k = u * 8;
-    int4 e = make_int4(0, 0, 1 << 20, 1 << 20);
+    int off = 0;
     if (k < kflat) {
       const int tap = k / w, ch = k - (k / w) * w;
       const int dy = tap / 3 - 1, dx = tap % 3 - 1;
-      e = make_int4(dy * W + dx, ch * 2, dy, dx);
+      off = dy * rowb + dx * q.astr + ch * 2;
     }
-    ktab[u] = e;
+    ktab[u] = off;
+  }
+  // zero the pad columns of both buffers once (staging and the epilogue only
+  // ever write interior pixels)
+  for (int i = tid; i < 2 * nrows * 2 * (q.astr >> 4); i += NT) {
+    const int per_row = 2 * (q.astr >> 4);
+    const int bsel = i / (nrows * per_row);
+    const int rem = i - bsel * nrows * per_row;
+    const int row = rem / per_row, cix = rem - (rem / per_row) * per_row;
+    const int side = cix / (q.astr >> 4), u = cix - side * (q.astr >> 4);
+    char* bb = bsel ? buf1 : buf0;
+    *reinterpret_cast<uint4*>(bb + row * rowb + (side ? (W + 1) : 0) * q.astr + u * 16) =
+        make_uint4(0, 0, 0, 0);
   }
   // copy channels [c0, c0+w) of image rows [ra, rb) into an LDS buffer.
-  // Thread t owns 16-B chunk t of every row (pixel t/cu, chunk t%cu, computed
-  // once); rows are unrolled 8-deep so each thread keeps 8 loads in flight.
+  // Thread t owns 16-B chunk t of every row (computed once); rows unrolled 8-deep.
   const int cu = w >> 3;
   const int rowchunks = W * cu;
-  const int my_px = tid / cu, my_u = tid - (tid / cu) * cu;
   auto stage_rows = [&](char* dst, int c0, int ra, int rb) __attribute__((always_inline)) {
-    for (int cbase = 0; cbase < rowchunks; cbase += NT) {
-      const int c = cbase + tid;
-      if (c >= rowchunks) break;
-      const int px = (cbase == 0) ? my_px : c / cu;
-      const int uu = (cbase == 0) ? my_u : c - (c / cu) * cu;
+    for (int c = tid; c < rowchunks; c += NT) {
+      const int px = c / cu, uu = c - (c / cu) * cu;
       const bf16_t* src = A + (img + px) * q.lda + c0 + uu * 8;
-      char* d = dst + px * q.astr + uu * 16;
+      char* d = dst + (px + 1) * q.astr + uu * 16;
       for (int row = ra; row < rb; row += 8) {
         uint4 v[8];
 #pragma unroll
@@ -962,59 +979,82 @@ __global__ __launch_bounds__(64 * NW) void split_chain(ChainParams q) {
         }
 #pragma unroll
         for (int r = 0; r < 8; ++r)
-          if (row + r < rb)
-            *reinterpret_cast<uint4*>(d + (row + r - rbase) * W * q.astr) = v[r];
+          if (row + r < rb) *reinterpret_cast<uint4*>(d + (row + r - rbase) * rowb) = v[r];
       }
     }
   };
   stage_rows(buf0, 0, r0 - nst, r0 + R + nst);
 
-  for (int k = 0; k < nst; ++k) {
-    // stage-k weights [BCO][kcp] (rows >= w are zero in the global layout)
-    {
-      const bf16_t* __restrict__ Wt = reinterpret_cast<const bf16_t*>(q.wt[k]);
-      const int total = BCO * units;
-      for (int b0 = tid; b0 < total; b0 += 8 * NT) {
-        uint4 v[8];
+  // weights of stage 0 straight into LDS
+  auto load_w = [&](int k, uint4 (&v)[WREG]) __attribute__((always_inline)) {
+    const bf16_t* __restrict__ Wt = reinterpret_cast<const bf16_t*>(q.wt[k]);
 #pragma unroll
-        for (int r = 0; r < 8; ++r) {
-          const int idx = b0 + r * NT;
-          const int rw = idx / units, u = idx - (idx / units) * units;
-          v[r] = (idx < total && u * 8 < kflat)
-                     ? *reinterpret_cast<const uint4*>(Wt + (size_t)rw * kflat + u * 8)
-                     : make_uint4(0, 0, 0, 0);
-        }
+    for (int r = 0; r < WREG; ++r) {
+      const int idx = tid + r * NT;
+      const int rw = idx / units, u = idx - (idx / units) * units;
+      v[r] = (idx < BCO * units && u * 8 < kflat)
+                 ? *reinterpret_cast<const uint4*>(Wt + (size_t)rw * kflat + u * 8)
+                 : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto store_w = [&](const uint4 (&v)[WREG]) __attribute__((always_inline)) {
 #pragma unroll
-        for (int r = 0; r < 8; ++r) {
-          const int idx = b0 + r * NT;
-          if (idx < total) {
-            const int rw = idx / units, u = idx - (idx / units) * units;
-            *reinterpret_cast<uint4*>(wts + rw * q.wstr + u * 16) = v[r];
-          }
-        }
+    for (int r = 0; r < WREG; ++r) {
+      const int idx = tid + r * NT;
+      if (idx < BCO * units) {
+        const int rw = idx / units, u = idx - (idx / units) * units;
+        *reinterpret_cast<uint4*>(wts + rw * q.wstr + u * 16) = v[r];
       }
     }
+  };
+  uint4 wr[WREG];
+  load_w(0, wr);
+  store_w(wr);
+  __syncthreads();
+
+  for (int k = 0; k < nst; ++k) {
     const int ext = nst - 1 - k;
     const int oa = r0 - ext, ob = r0 + R + ext;     // output image rows of this stage
     char* in = (k & 1) ? buf1 : buf0;
     char* out = (k & 1) ? buf0 : buf1;
-    if (k + 1 < nst) stage_rows(out, (k + 1) * w, oa, ob);
-    __syncthreads();
+    const bool more = k + 1 < nst;
+    // prefetch x_{k+1} rows [oa, ob) and the next stage's weights into
+    // registers; they land while this stage computes
+    const int xchunks = (ob - oa) * rowchunks;
+    uint4 xr[XREG];
+    if (more) {
+#pragma unroll
+      for (int r = 0; r < XREG; ++r) {
+        const int c = tid + r * NT;
+        xr[r] = make_uint4(0, 0, 0, 0);
+        if (c < xchunks) {
+          const int rr = oa + c / rowchunks;
+          const int cc = c - (c / rowchunks) * rowchunks;
+          const int px = cc / cu, uu = cc - (cc / cu) * cu;
+          if (rr >= 0 && rr < H)
+            xr[r] = *reinterpret_cast<const uint4*>(A + (img + (size_t)rr * W + px) * q.lda +
+                                                    (k + 1) * w + uu * 8);
+        }
+      }
+      load_w(k + 1, wr);
+    }
     const float* __restrict__ bm = q.mean[k];
     const float* __restrict__ bi = q.inv[k];
     const int npix = (ob - oa) * W;
     const int ntiles = (npix + 15) >> 4;
+    const char* wrow = wts + col * q.wstr + 16 * g;
     for (int t0 = wave * WPX; t0 < ntiles; t0 += NW * WPX) {
-      int prow[WPX], pcol[WPX];
+      int prow[WPX], pcol[WPX], base[WPX];
       bool pv[WPX];
 #pragma unroll
       for (int j = 0; j < WPX; ++j) {
         const int lp = (t0 + j) * 16 + col;
         pv[j] = lp < npix;
-        const int l = pv[j] ? lp : 0;
+        const int l = pv[j] ? lp : npix - 1;       // clamp: reads stay in the buffer
         prow[j] = oa + l / W;
         pcol[j] = l - (l / W) * W;
         pv[j] = pv[j] && prow[j] >= 0 && prow[j] < H;
+        base[j] = (prow[j] - rbase) * rowb + (pcol[j] + 1) * q.astr;
       }
       f32x4 acc[WCO][WPX];
 #pragma unroll
@@ -1022,25 +1062,19 @@ __global__ __launch_bounds__(64 * NW) void split_chain(ChainParams q) {
 #pragma unroll
         for (int j = 0; j < WPX; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
       for (int k0 = 0; k0 < q.kcp; k0 += 32) {
-        const int4 e = ktab[(k0 >> 3) + g];
+        const int off = ktab[(k0 >> 3) + g];
         bf16x8 a[WCO], b[WPX];
 #pragma unroll
         for (int i = 0; i < WCO; ++i)
-          a[i] = *reinterpret_cast<const bf16x8*>(wts + (16 * i + col) * q.wstr + (k0 + 8 * g) * 2);
+          a[i] = *reinterpret_cast<const bf16x8*>(wrow + 16 * i * q.wstr + k0 * 2);
 #pragma unroll
-        for (int j = 0; j < WPX; ++j) {
-          const int yy = prow[j] + e.z, xx = pcol[j] + e.w;
-          const bool ok = pv[j] && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
-          b[j] = ok ? *reinterpret_cast<const bf16x8*>(
-                          in + ((prow[j] - rbase) * W + pcol[j] + e.x) * q.astr + e.y)
-                    : bf16x8{};
-        }
+        for (int j = 0; j < WPX; ++j) b[j] = *reinterpret_cast<const bf16x8*>(in + base[j] + off);
 #pragma unroll
         for (int i = 0; i < WCO; ++i)
 #pragma unroll
           for (int j = 0; j < WPX; ++j) acc[i][j] = mfma_step(a[i], b[j], acc[i][j]);
       }
-      // epilogue: y = relu(bn(acc)) -> HBM (central rows) and z_{k+1} += y in LDS
+      // epilogue: y = relu(bn(acc)) -> HBM (central rows) and -> LDS (next input)
 #pragma unroll
       for (int i = 0; i < WCO; ++i) {
         const int co = 16 * i + 4 * g;
@@ -1055,17 +1089,34 @@ __global__ __launch_bounds__(64 * NW) void split_chain(ChainParams q) {
           for (int r = 0; r < 4; ++r) y[r] = (bf16_t)fmaxf((acc[i][j][r] - m[r]) * sc[r], 0.f);
           if (prow[j] >= r0 && prow[j] < r0 + R)
             *reinterpret_cast<bf16x4*>(Bo + (img + (size_t)prow[j] * W + pcol[j]) * q.ldb + k * w + co) = y;
-          if (k + 1 < nst) {
-            bf16x4* zp = reinterpret_cast<bf16x4*>(out + ((prow[j] - rbase) * W + pcol[j]) * q.astr + co * 2);
-            bf16x4 x = *zp, z;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) z[r] = (bf16_t)((float)x[r] + (float)y[r]);
-            *zp = z;
-          }
+          if (more) *reinterpret_cast<bf16x4*>(out + base[j] + co * 2) = y;
         }
       }
     }
     __syncthreads();
+    if (more) {
+      // combine pass: z_{k+1} = x_{k+1} + y_k (bf16, as the unfused path);
+      // rows outside the image stay zero
+#pragma unroll
+      for (int r = 0; r < XREG; ++r) {
+        const int c = tid + r * NT;
+        if (c < xchunks) {
+          const int rr = oa + c / rowchunks;
+          const int cc = c - (c / rowchunks) * rowchunks;
+          const int px = cc / cu, uu = cc - (cc / cu) * cu;
+          uint4* zp = reinterpret_cast<uint4*>(out + (rr - rbase) * rowb + (px + 1) * q.astr + uu * 16);
+          if (rr >= 0 && rr < H) {
+            const bf16x8 x = __builtin_bit_cast(bf16x8, xr[r]);
+            const bf16x8 y = __builtin_bit_cast(bf16x8, *zp);
+            *zp = __builtin_bit_cast(uint4, frag_add(x, y));
+          } else {
+            *zp = make_uint4(0, 0, 0, 0);  // SAME zero padding of the next stage
+          }
+        }
+      }
+      store_w(wr);
+      __syncthreads();
+    }
   }
 }
 
@@ -1093,6 +1144,76 @@ hipError_t launch_split_chain(const ChainParams& q, int wco, int wpx, hipStream_
   }
 #undef CH_CASE
   return hipErrorInvalidValue;
+}
+
+// ----------------------------------------------------------------------------
+// Stem: 3x3 SAME conv from one input channel (res2net_model.py:192-203,
+// dpn_model.py:113) + BN + ReLU.  One thread per output pixel, all Cout
+// channels 8 at a time, weights (bf16-rounded in bf16 mode, like the MFMA
+// path) and BN in LDS.  Reads the fp32 features directly; in bf16 mode each
+// tap is rounded to bf16 first, exactly as the separate cast would.
+template <typename T>
+__global__ __launch_bounds__(256) void stem_conv1(const float* __restrict__ x, int N, int H,
+                                                  int W, const float* __restrict__ wts, int Cout,
+                                                  const float* __restrict__ mean,
+                                                  const float* __restrict__ inv,
+                                                  T* __restrict__ y) {
+  __shared__ float sw[9 * 64];
+  __shared__ float sm[64], si[64];
+  for (int i = threadIdx.x; i < 9 * Cout; i += blockDim.x) sw[i] = wts[i];
+  for (int i = threadIdx.x; i < Cout; i += blockDim.x) { sm[i] = mean[i]; si[i] = inv[i]; }
+  __syncthreads();
+  const int64_t pix = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (pix >= (int64_t)N * H * W) return;
+  const int wi = (int)(pix % W);
+  const int hi = (int)((pix / W) % H);
+  float v[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int yy = hi + t / 3 - 1, xx = wi + t % 3 - 1;
+    float a = (yy >= 0 && yy < H && xx >= 0 && xx < W) ? x[pix + (t / 3 - 1) * W + (t % 3 - 1)] : 0.f;
+    if constexpr (sizeof(T) == 2) a = (float)(bf16_t)a;
+    v[t] = a;
+  }
+  T* out = y + pix * Cout;
+  for (int c0 = 0; c0 < Cout; c0 += 8) {
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = min(c0 + e, Cout - 1);
+      float sacc = 0.f;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) sacc = fmaf(v[t], sw[t * Cout + c], sacc);
+      acc[e] = fmaxf((sacc - sm[c]) * si[c], 0.f);
+    }
+    if (c0 + 8 <= Cout && (Cout % 8) == 0) {
+      if constexpr (sizeof(T) == 2) {
+        bf16x8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = (bf16_t)acc[e];
+        *reinterpret_cast<uint4*>(out + c0) = __builtin_bit_cast(uint4, o);
+      } else {
+        *reinterpret_cast<f32x4*>(out + c0) = f32x4{acc[0], acc[1], acc[2], acc[3]};
+        *reinterpret_cast<f32x4*>(out + c0 + 4) = f32x4{acc[4], acc[5], acc[6], acc[7]};
+      }
+    } else {
+      for (int e = 0; e < 8 && c0 + e < Cout; ++e) out[c0 + e] = (T)acc[e];
+    }
+  }
+}
+
+hipError_t launch_stem(DType t, const float* x, int N, int H, int W, const float* wts, int Cout,
+                       const float* mean, const float* inv, void* y, hipStream_t s) {
+  if (Cout > 64) return hipErrorInvalidValue;
+  const int64_t n = (int64_t)N * H * W;
+  const unsigned g = (unsigned)((n + 255) / 256);
+  if (t == BF16)
+    hipLaunchKernelGGL(stem_conv1<bf16_t>, dim3(g), dim3(256), 0, s, x, N, H, W, wts, Cout, mean,
+                       inv, (bf16_t*)y);
+  else
+    hipLaunchKernelGGL(stem_conv1<float>, dim3(g), dim3(256), 0, s, x, N, H, W, wts, Cout, mean,
+                       inv, (float*)y);
+  return hipGetLastError();
 }
 
 int conv_kstep(DType t) { return t == BF16 ? Tr<bf16_t>::KSTEP : Tr<float>::KSTEP; }
@@ -1306,8 +1427,43 @@ __global__ __launch_bounds__(256) void avgpool3s2_k(const T* __restrict__ x, int
   y[pix * ldy + c] = (T)(s / 9.0f);
 }
 
+// bf16, C % 8 == 0: 8 channels per thread with 16-byte loads/stores (same sum order)
+__global__ __launch_bounds__(256) void avgpool3s2_v8(const bf16_t* __restrict__ x, int ldx, int N,
+                                                     int H, int W, int C8, bf16_t* __restrict__ y,
+                                                     int ldy, int Ho, int Wo) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)N * Ho * Wo * C8) return;
+  const int c = (int)(idx % C8) * 8;
+  const int64_t pix = idx / C8;
+  const int wo = (int)(pix % Wo);
+  const int ho = (int)((pix / Wo) % Ho);
+  const int n = (int)(pix / ((int64_t)Wo * Ho));
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int ky = 0; ky < 3; ++ky) {
+    const int hi = 2 * ho - 1 + ky;
+    if (hi < 0 || hi >= H) continue;
+    for (int kx = 0; kx < 3; ++kx) {
+      const int wi = 2 * wo - 1 + kx;
+      if (wi < 0 || wi >= W) continue;
+      const bf16x8 v = ld16(x + (((size_t)n * H + hi) * W + wi) * ldx + c);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s[e] += (float)v[e];
+    }
+  }
+  bf16x8 o;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o[e] = (bf16_t)(s[e] / 9.0f);
+  *reinterpret_cast<uint4*>(y + pix * ldy + c) = __builtin_bit_cast(uint4, o);
+}
+
 hipError_t launch_avgpool3s2(DType t, const void* x, int ldx, int N, int H, int W, int C,
                              void* y, int ldy, int Ho, int Wo, hipStream_t s) {
+  if (t == BF16 && C % 8 == 0 && ldx % 8 == 0 && ldy % 8 == 0) {
+    const int64_t n = (int64_t)N * Ho * Wo * (C / 8);
+    hipLaunchKernelGGL(avgpool3s2_v8, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                       (const bf16_t*)x, ldx, N, H, W, C / 8, (bf16_t*)y, ldy, Ho, Wo);
+    return hipGetLastError();
+  }
   const int64_t n = (int64_t)N * Ho * Wo * C;
   const unsigned g = (unsigned)((n + 255) / 256);
   if (t == BF16)
