@@ -177,18 +177,37 @@ def test_extract_cli_end_to_end(weights, tmp_path):
     assert len(open(tmp_path / "xv.scp").read().splitlines()) == len(mats)
 
 
-@pytest.mark.parametrize("name,F,T", [("res2net50_w24_s4_c32", 80, 200), ("res2net50_w24_s4_c32", 80, 37),
-                                      ("res2net50_w8_s6_c16", 40, 64)])
-def test_fused_kernels_bitwise_equal_unfused(weights, name, F, T, monkeypatch):
-    """The fused split chain and the specialised 1x1/window kernels compute the
-    same bf16 arithmetic as the generic path: embeddings must be identical
-    (VOXEMB_NO_* are read at model load)."""
+@pytest.mark.parametrize("unfused_env", [("VOXEMB_NO_BNECK",), ("VOXEMB_NO_BNECK", "VOXEMB_NO_CHAIN")],
+                         ids=["chain", "unfused"])
+@pytest.mark.parametrize("name,F,T,N", [("res2net50_w24_s4_c32", 80, 200, 3),
+                                        ("res2net50_w24_s4_c32", 80, 37, 3),
+                                        ("res2net50_w24_s4_c32", 40, 75, 2),
+                                        ("res2net50_w8_s6_c16", 40, 64, 3)])
+def test_fused_kernels_bitwise_equal_unfused(weights, name, F, T, N, unfused_env, monkeypatch):
+    """The fused bottleneck / split chain and the specialised 1x1/window
+    kernels compute the same bf16 arithmetic as the generic path: embeddings
+    must be identical (VOXEMB_NO_* are read at model load)."""
     from voxsrc2020_speaker_verification_amd import synth
     spec, t, blob = weights(name, F)
-    x = synth.make_features(3, T, F, seed=21)
+    x = synth.make_features(N, T, F, seed=21)
     with _extractor(blob, "bf16") as ex:
         fused = ex.run(x)
-    monkeypatch.setenv("VOXEMB_NO_CHAIN", "1")
+    for k in unfused_env:
+        monkeypatch.setenv(k, "1")
     with _extractor(blob, "bf16") as ex:
         unfused = ex.run(x)
     assert np.array_equal(fused, unfused)
+
+
+def test_bneck_segments_bitwise(weights, monkeypatch):
+    """Row segmentation of the fused bottleneck (N=1 -> many segments, warm-up
+    rows recomputed) gives the same bits as one segment per utterance."""
+    import torch
+    from voxsrc2020_speaker_verification_amd import synth
+    spec, t, blob = weights("res2net50_w24_s4_c32", 80)
+    x = synth.make_features(4, 150, 80, seed=5)
+    with _extractor(blob, "bf16") as ex:
+        full = ex.run(x)
+        assert any(l.startswith("bneck") for l in ex.describe(torch.from_numpy(x).cuda()))
+        for i in range(4):
+            assert np.array_equal(ex.run(x[i:i + 1])[0], full[i])

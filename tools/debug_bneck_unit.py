@@ -1,0 +1,137 @@
+"""One fused identity bottleneck (bneck.hip) on random data vs a numpy
+emulation with the same bf16 rounding points (GPU debug tool).
+
+usage: python tools/debug_bneck_unit.py [H] [W] [variant]
+variant: full | zero_chain | only_x4 (1x1c reads only the passthrough plane)
+"""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.getcwd())
+from voxsrc2020_speaker_verification_amd import _native  # noqa: E402
+
+
+def bf16(a):
+    a = np.ascontiguousarray(a, np.float32)
+    u = a.view(np.uint32).astype(np.uint64)
+    u = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16) << 16
+    return u.astype(np.uint32).view(np.float32)
+
+
+class BneckParams(C.Structure):
+    _fields_ = [("x", C.c_void_p), ("y", C.c_void_p),
+                ("N", C.c_int), ("H", C.c_int), ("W", C.c_int), ("seg", C.c_int), ("nseg", C.c_int),
+                ("wa", C.c_void_p), ("ma", C.c_void_p), ("ia", C.c_void_p),
+                ("wb", C.c_void_p * 8), ("mb", C.c_void_p * 8), ("ib", C.c_void_p * 8),
+                ("wc", C.c_void_p), ("mc", C.c_void_p), ("ic", C.c_void_p)]
+
+
+def paired(wio):
+    """[cin][cout] -> paired-row [cout][cin] (row (2q+u)*16+4g+e <- channel 32q+8g+4u+e)."""
+    cin, cout = wio.shape
+    out = np.zeros((cout, cin), np.float32)
+    for row in range(cout):
+        q, u, g, e = row // 32, (row // 16) & 1, (row & 15) // 4, row & 3
+        out[row] = wio[:, 32 * q + 8 * g + 4 * u + e]
+    return out
+
+
+def conv3x3_same(x, k):   # x [H][W][ci], k [3][3][ci][co]
+    H, W, _ = x.shape
+    xp = np.pad(x, ((1, 1), (1, 1), (0, 0)))
+    out = np.zeros((H, W, k.shape[3]), np.float32)
+    for ky in range(3):
+        for kx in range(3):
+            out += xp[ky:ky + H, kx:kx + W] @ k[ky, kx]
+    return out
+
+
+def main():
+    H = int(sys.argv[1]) if len(sys.argv) > 1 else 40
+    W = int(sys.argv[2]) if len(sys.argv) > 2 else 80
+    variant = sys.argv[3] if len(sys.argv) > 3 else "full"
+    N = int(sys.argv[4]) if len(sys.argv) > 4 else 1
+    nseg = int(sys.argv[5]) if len(sys.argv) > 5 else 1
+    Cc, w, S = 128, 24, 4
+    SW = S * w
+    rng = np.random.default_rng(0)
+    X = bf16(rng.standard_normal((N, H, W, Cc)))
+    Wa = bf16(rng.standard_normal((Cc, SW)) / np.sqrt(Cc))
+    Wb = [bf16(rng.standard_normal((3, 3, w, w)) / np.sqrt(9 * w)) for _ in range(S - 1)]
+    Wc = bf16(rng.standard_normal((SW, Cc)) / np.sqrt(SW))
+    if variant == "zero_chain":
+        Wb = [np.zeros_like(k) for k in Wb]
+    if variant == "only_x4":
+        Wc[: (S - 1) * w] = 0
+    ma = rng.standard_normal(SW).astype(np.float32) * 0.1
+    ia = (1 + rng.random(SW)).astype(np.float32)
+    mb = [rng.standard_normal(w).astype(np.float32) * 0.1 for _ in range(S - 1)]
+    ib = [(1 + rng.random(w)).astype(np.float32) for _ in range(S - 1)]
+    mc = rng.standard_normal(Cc).astype(np.float32) * 0.1
+    ic = (1 + rng.random(Cc)).astype(np.float32)
+
+    # numpy emulation (rounding points of the unfused path)
+    refs = []
+    for i in range(N):
+        Xi = X[i]
+        x = bf16(np.maximum((Xi @ Wa - ma) * ia, 0))
+        ys, prev = [], None
+        for k in range(S - 1):
+            xk = x[..., k * w:(k + 1) * w]
+            z = xk if prev is None else bf16(xk + prev)
+            y = bf16(np.maximum((conv3x3_same(z, Wb[k]) - mb[k]) * ib[k], 0))
+            ys.append(y)
+            prev = y
+        cat = np.concatenate(ys + [x[..., (S - 1) * w:]], -1)
+        refs.append(bf16(np.maximum((cat @ Wc - mc) * ic + Xi, 0)))
+    ref = np.stack(refs)
+
+    dev = "cuda"
+    tb = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(dev).to(torch.bfloat16)
+    tf = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(dev)
+    xd = tb(X)
+    yd = torch.zeros_like(xd)
+    wa_d = tb(paired(Wa))
+    wc_d = tb(paired(Wc))
+    wb_d = []
+    for k in range(S - 1):
+        h = np.zeros((32, 9 * w), np.float32)
+        for co in range(w):
+            for t in range(9):
+                h[co, t * w:(t + 1) * w] = Wb[k][t // 3, t % 3, :, co]
+        wb_d.append(tb(h))
+    keep = [tf(ma), tf(ia), tf(mc), tf(ic)] + [tf(a) for a in mb] + [tf(a) for a in ib]
+    q = BneckParams()
+    q.x, q.y = xd.data_ptr(), yd.data_ptr()
+    q.N, q.H, q.W = N, H, W
+    q.seg = (H + nseg - 1) // nseg
+    q.nseg = (H + q.seg - 1) // q.seg
+    q.wa, q.ma, q.ia = wa_d.data_ptr(), keep[0].data_ptr(), keep[1].data_ptr()
+    for k in range(S - 1):
+        q.wb[k] = wb_d[k].data_ptr()
+        q.mb[k] = keep[4 + k].data_ptr()
+        q.ib[k] = keep[4 + S - 1 + k].data_ptr()
+    q.wc, q.mc, q.ic = wc_d.data_ptr(), keep[2].data_ptr(), keep[3].data_ptr()
+    lib = _native.lib()
+    fn = getattr(lib, "_ZN3vox12launch_bneckERKNS_11BneckParamsEiiiP12ihipStream_t")
+    fn.restype = C.c_int
+    fn.argtypes = [C.POINTER(BneckParams), C.c_int, C.c_int, C.c_int, C.c_void_p]
+    rc = fn(C.byref(q), Cc, w, S, None)
+    torch.cuda.synchronize()
+    print("launch rc", rc)
+    got = yd.float().cpu().numpy()
+    d = np.abs(got - ref)
+    print(f"{variant}: max|diff| {d.max():.4g}  mean {d.mean():.4g}  exact {np.mean(d == 0):.4f}")
+    bad = np.argwhere(d > 0.05 * (1 + np.abs(ref)))
+    if len(bad):
+        for name, ax in (("utt", 0), ("rows", 1), ("cols", 2), ("chans", 3)):
+            u = np.unique(bad[:, ax])
+            print("bad", name, u[:40], "n", len(u))
+
+
+if __name__ == "__main__":
+    main()

@@ -14,6 +14,7 @@ ARCH = os.environ.get("VOX_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = [
     ("kernels.hip", ["-O3"]),
+    ("bneck.hip", ["-O3"]),
     ("api.cpp", ["-O2"]),
     ("kaldi_host.cpp", ["-O2", "-ffp-contract=off"]),
 ]
@@ -30,23 +31,27 @@ def build(verbose=False, force=False) -> str:
     outdir = os.path.join(HERE, "..", "build", "native")
     os.makedirs(outdir, exist_ok=True)
     hipcc = _hipcc()
-    objs = []
-    newest_src = 0.0
-    for name in os.listdir(CSRC):
-        newest_src = max(newest_src, os.path.getmtime(os.path.join(CSRC, name)))
     hdr = os.path.join(HERE, "..", "include", "voxemb.h")
-    newest_src = max(newest_src, os.path.getmtime(hdr), os.path.getmtime(__file__))
-    if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= newest_src:
-        return LIB
+    newest_hdr = max([os.path.getmtime(hdr), os.path.getmtime(__file__)] +
+                     [os.path.getmtime(os.path.join(CSRC, n)) for n in os.listdir(CSRC)
+                      if n.endswith(".h")])
+    objs, relink = [], force or not os.path.exists(LIB)
     for src, flags in SOURCES:
+        path = os.path.join(CSRC, src)
         obj = os.path.join(outdir, src + ".o")
+        objs.append(obj)
+        if (not force and os.path.exists(obj) and
+                os.path.getmtime(obj) >= max(newest_hdr, os.path.getmtime(path))):
+            continue
         lang = ["-x", "hip"] if src.endswith(".hip") else []
         cmd = [hipcc, f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-c", *lang,
-               os.path.join(CSRC, src), "-o", obj, *flags]
+               path, "-o", obj, *flags]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)
-        objs.append(obj)
+        relink = True
+    if not relink and all(os.path.getmtime(LIB) >= os.path.getmtime(o) for o in objs):
+        return LIB
     cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs]
     subprocess.run(cmd, check=True)
     return LIB

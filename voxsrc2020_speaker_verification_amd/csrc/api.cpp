@@ -188,6 +188,7 @@ struct Op {
              Ho = 0, Wo = 0;
   int64_t count = 0;
   ChainParams ch{};
+  BneckParams bq{};  // type 12: C, w (cl.wco), split (S)
   double flops = 0, bytes = 0;
 };
 
@@ -219,6 +220,8 @@ struct vox_model {
   bool no_gemm = false;        // VOXEMB_NO_GEMM=1: disable gemm1x1_lds
   bool no_chain = false;       // VOXEMB_NO_CHAIN=1: unfused Res2Net branches
   bool no_stem = false;        // VOXEMB_NO_STEM=1: stem through the generic conv
+  bool no_bneck = false;       // VOXEMB_NO_BNECK=1: unfused identity bottlenecks
+  int bneck_nseg = 0;          // VOXEMB_BNECK_NSEG: force row segments per utterance (tests)
   int chain_r = 0, chain_wpx = 0, chain_nw = 0;  // VOXEMB_CHAIN_R / VOXEMB_CHAIN_WPX (tuning)
   int rr_wpx = 0, rr_wco = 0;  // VOXEMB_RR_WPX / VOXEMB_RR_WCO: tile overrides (tuning)
 };
@@ -720,6 +723,47 @@ static int build_res2net(Builder& B, const float* x, int n, int t, float* out) {
     for (int b = 0; b < blocks[st]; ++b) {
       const int stride = b == 0 ? strides[st] : 1;
       const int Ho = (H + stride - 1) / stride, Wo = (W + stride - 1) / stride;
+      if (stride == 1 && b > 0 && m->dt == BF16 && !m->no_bneck && cur.ld == cur.C &&
+          bneck_lds(cur.C, w, s, W) > 0) {
+        // whole identity bottleneck in one launch (bneck.hip)
+        const ConvW& c1a = m->convs[ci];
+        const ConvW& c1c = m->convs[ci + s];
+        bool ok = s - 1 <= 8 && c1a.wpair && c1c.wpair && c1a.cin == cur.C && c1a.cout == sw &&
+                  c1c.cin == sw && c1c.cout == cur.C && c1a.mean && c1c.mean;
+        for (int j = 0; ok && j < s - 1; ++j)
+          ok = m->convs[ci + 1 + j].wtc != nullptr && m->convs[ci + 1 + j].coutp >= 16 * ((w + 15) / 16);
+        if (ok) {
+          BneckParams q{};
+          void* yo = B.base(nxt_s, (size_t)n * H * W * cur.C * es);
+          q.x = cur.p; q.y = yo; q.N = n; q.H = H; q.W = W;
+          // one workgroup per CU: split utterances into row segments until the
+          // grid covers the chip (segments keep >= 16 rows; 2(s-1) warm-up rows each)
+          int nseg = 1;
+          while (n * nseg < 256 && H / (2 * nseg) >= 16) nseg *= 2;
+          if (m->bneck_nseg > 0) nseg = std::min(m->bneck_nseg, H);
+          q.seg = (H + nseg - 1) / nseg;
+          q.nseg = (H + q.seg - 1) / q.seg;
+          q.wa = c1a.wpair->p; q.ma = (const float*)c1a.mean->p; q.ia = (const float*)c1a.inv->p;
+          for (int j = 0; j < s - 1; ++j) {
+            const ConvW& br = m->convs[ci + 1 + j];
+            q.wb[j] = br.wtc->p; q.mb[j] = (const float*)br.mean->p; q.ib[j] = (const float*)br.inv->p;
+          }
+          q.wc = c1c.wpair->p; q.mc = (const float*)c1c.mean->p; q.ic = (const float*)c1c.inv->p;
+          Op op;
+          op.kind = OP_CONV;
+          op.type = 12;
+          op.bq = q;
+          op.C = cur.C; op.cl.wco = w; op.S = s;
+          const double px = (double)n * H * W;
+          op.flops = 2.0 * px * ((double)cur.C * sw + (s - 1) * 9.0 * w * w + (double)sw * cur.C);
+          op.bytes = (double)es * px * cur.C * 2.0;
+          B.ops->push_back(op);
+          ci += s + 1;
+          cur = Act{yo, cur.C, n, H, W, cur.C};
+          std::swap(cur_s, nxt_s);
+          continue;
+        }
+      }
       const void* shortcut = cur.p;
       int ld_sc = cur.ld;
       if (b == 0) {  // projection_shortcut: 1x1 stride s, no pad, + BN (:85-87,125-127)
@@ -945,6 +989,7 @@ static hipError_t run_op(vox_model* m, const Op& op, hipStream_t s) {
     case 8: return launch_conv1x1_rr(op.cp, op.cl, s);
     case 9: return launch_gemm1x1(op.cp, s);
     case 10: return launch_split_chain(op.ch, op.cl.wco, op.cl.wpx, s);
+    case 12: return launch_bneck(op.bq, op.C, op.cl.wco, op.S, s);
     case 11:
       return launch_stem(m->dt, (const float*)op.src, op.N, op.H, op.W, op.part, op.C, op.mean,
                          op.inv, op.dst, s);
@@ -1006,6 +1051,8 @@ extern "C" int vox_load_blob(const void* blob, size_t nbytes, int device, int pr
   if (const char* e = std::getenv("VOXEMB_NO_GEMM")) m->no_gemm = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_NO_CHAIN")) m->no_chain = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_NO_STEM")) m->no_stem = std::atoi(e) != 0;
+  if (const char* e = std::getenv("VOXEMB_NO_BNECK")) m->no_bneck = std::atoi(e) != 0;
+  if (const char* e = std::getenv("VOXEMB_BNECK_NSEG")) m->bneck_nseg = std::atoi(e);
   if (const char* e = std::getenv("VOXEMB_CHAIN_R")) m->chain_r = std::atoi(e);
   if (const char* e = std::getenv("VOXEMB_CHAIN_WPX")) m->chain_wpx = std::atoi(e);
   if (const char* e = std::getenv("VOXEMB_CHAIN_NW")) m->chain_nw = std::atoi(e);
@@ -1135,6 +1182,8 @@ extern "C" int vox_profile(vox_model* m, const float* d_x, int n, int t, int f, 
         tag |= (o.cl.wco << 4) | (o.cl.wpx << 8) | (1 << 22);
       else if (o.type == 11)
         tag |= (1 << 23);
+      else if (o.type == 12)
+        tag |= (1 << 24);
       else if (o.type == 8)
         tag |= (o.cl.wco << 4) | (o.cl.wpx << 8) | (((o.cp.cinp + 31) / 32) << 16) | (1 << 20);
       else if (o.type == 0 || o.type == 5)
@@ -1156,7 +1205,7 @@ extern "C" int vox_plan_describe(vox_model* m, const float* d_x, int n, int t, i
   if ((rc = ensure_plan(m, d_x, n, t, (float*)m->stage_out.p))) return rc;
   std::string out;
   static const char* tn[] = {"igemm", "reduce", "pool", "avgpool", "convert", "igemm32", "bnrelu",
-                             "win", "rr", "gemm", "chain", "stem"};
+                             "win", "rr", "gemm", "chain", "stem", "bneck"};
   for (const Op& o : m->plan) {
     char line[256];
     const ConvParams& p = o.cp;
@@ -1167,6 +1216,9 @@ extern "C" int vox_plan_describe(vox_model* m, const float* d_x, int n, int t, i
                     tn[o.type], o.cl.wco, o.cl.wpx, o.cl.splitk, p.N, p.H, p.W, p.Cin, p.Ho, p.Wo,
                     p.Cout, p.kh, p.kw, p.sh, p.groups, p.flags, p.x2 ? 1 : 0, p.in_mean ? 1 : 0,
                     o.flops, o.bytes);
+    else if (o.type == 12)
+      std::snprintf(line, sizeof(line), "bneck N=%d H=%d W=%d C=%d w=%d split=%d seg=%d nseg=%d flops=%.4g bytes=%.4g\n",
+                    o.bq.N, o.bq.H, o.bq.W, o.C, o.cl.wco, o.S, o.bq.seg, o.bq.nseg, o.flops, o.bytes);
     else if (o.type == 10)
       std::snprintf(line, sizeof(line), "chain wco=%d wpx=%d N=%d H=%d W=%d w=%d nst=%d R=%d lds=%d flops=%.4g bytes=%.4g\n",
                     o.cl.wco, o.cl.wpx, o.ch.N, o.ch.H, o.ch.W, o.ch.w, o.ch.nst, o.ch.R, o.ch.lds,

@@ -1,0 +1,381 @@
+// Fused Res2Net identity bottleneck (stride 1, identity shortcut), bf16:
+//
+//   x   = relu(bn_a(conv1x1_a(in)))                  split into S planes x_1..x_S
+//   y_1 = relu(bn_1(conv3x3_1(x_1)))
+//   y_k = relu(bn_k(conv3x3_k(x_k + y_{k-1})))       k = 2..S-1
+//   out = relu(bn_c(conv1x1_c([y_1 .. y_{S-1}, x_S])) + in)
+//
+// (res2net_model.py:26-103, one `block` with stype 'normal'.)  The unfused
+// path moves every intermediate through HBM three times (1x1a -> split chain
+// -> 1x1c, ~1.5 KB per pixel at 128 channels); here a workgroup streams one
+// utterance segment row by row (time = image rows) and keeps every
+// intermediate in LDS ring buffers, so HBM sees the block input once and the
+// block output once (~0.5 KB per pixel).
+//
+// Row pipeline, step t handles A-row a = h0-(S-1)+t:
+//   phase 0   : 1x1a on row a (input row staged in LDS)     -> rings x_1..x_S
+//               1x1c on row a-S (rings y_1..y_{S-1}, x_S)    -> HBM (+ residual)
+//   phase k   : 3x3 stage k on row a-k (ring z_k rows a-k-1..a-k+1)
+//               -> ring y_k, and z_{k+1} = x_{k+1} + y_k (bf16, as unfused)
+// Ring depths follow from the lags: z_k 3 rows, x_k k rows, x_S S+1 rows,
+// y_k S-k rows.  Rows outside the image are zero (SAME padding).  Segments
+// recompute 2(S-1) warm-up rows.
+//
+// Work split (8 waves): phase 0 -- waves 0..NPA-1 own one 32-channel pair of
+// 1x1a outputs, waves NW-NPC..NW-1 one pair of 1x1c outputs, each across all
+// pixel tiles, with that pair's weights held in registers for the whole
+// kernel; chain phases -- wave w owns cout tile w % WCO of every stage (its
+// weights in registers) and pixel tiles w/WCO, w/WCO + NW/WCO, ...
+// Accumulation orders (K chunks of 32, paired-row 1x1 weights, flattened
+// tap-major 3x3 K) equal the unfused kernels', so results are bit-identical.
+#include "kernels.h"
+#include "device_common.h"
+
+namespace vox {
+
+template <int C, int WID, int S, int PT>
+struct BneckCfg {
+  static constexpr int NW = 8, NT = 64 * NW;
+  static constexpr int SW = S * WID;
+  static constexpr int NPA = SW / 32, KSA = C / 32;  // 1x1a: output pairs, k-steps
+  static constexpr int NPC = C / 32, KSC = SW / 32;  // 1x1c
+  static constexpr int KSW = KSA > KSC ? KSA : KSC;
+  static constexpr int WCO = (WID + 15) / 16;        // 3x3 cout tiles
+  static constexpr int KFLAT = 9 * WID;
+  static constexpr int KCP = (KFLAT + 31) / 32 * 32;
+  static constexpr int KST = KCP / 32;
+  static constexpr int AU = ((WID / 8) & 1) ? WID / 8 : WID / 8 + 1;  // odd 16-B units
+  static constexpr int ASTR = AU * 16;                                // ring pixel stride
+  static constexpr int IU = ((C / 8) & 1) ? C / 8 : C / 8 + 1;
+  static constexpr int ISTR = IU * 16;                                // input-row pixel stride
+  static constexpr int WR = 16 * PT + 2;  // ring row: pad | pixels | pad (+ tile slack)
+  static constexpr int ROWB = WR * ASTR;
+  // ring planes (one image row each)
+  static constexpr int ZB(int k) { return 3 * (k - 1); }              // z_k, k = 1..S-1
+  static constexpr int ZEND = 3 * (S - 1);
+  static constexpr int XB(int k) { return ZEND + (k - 1) * k / 2 - 1; }  // x_k, k = 2..S
+  static constexpr int XEND = XB(S) + S + 1;
+  static constexpr int YB(int k) { return XEND + (k - 1) * S - (k - 1) * k / 2; }  // y_k
+  static constexpr int NPLANES = XEND + S * (S - 1) / 2;
+  static constexpr int RING_BYTES = NPLANES * ROWB;
+  static constexpr int IN_BYTES = 16 * PT * ISTR;
+  static constexpr int BN_FLOATS = 2 * (S - 1) * 16 * WCO + 2 * SW + 2 * C;
+  static constexpr int LDS = RING_BYTES + IN_BYTES + 4 * BN_FLOATS;
+  static constexpr int CU = C / 8;                            // 16-B chunks per input pixel
+  static constexpr int IREG = (16 * PT * CU + NT - 1) / NT;   // input-row chunks per thread
+};
+
+// ring slot of image row r (r >= -840) in a ring of `depth` rows
+template <int D> __device__ __forceinline__ int slot(int r) { return (r + 840) % D; }
+
+__device__ __forceinline__ bf16x4 add4(bf16x4 a, bf16x4 b) {
+  bf16x4 r;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) r[e] = (bf16_t)((float)a[e] + (float)b[e]);
+  return r;
+}
+
+template <int C, int WID, int S, int PT>
+__global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
+  using K = BneckCfg<C, WID, S, PT>;
+  constexpr int NW = K::NW, NT = K::NT, WCO = K::WCO, KST = K::KST;
+  constexpr int ASTR = K::ASTR, ROWB = K::ROWB;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int col = lane & 15, g = lane >> 4;
+  const int H = q.H, W = q.W;
+  const int n = blockIdx.x / q.nseg;
+  const int h0 = (blockIdx.x - n * q.nseg) * q.seg;
+  const int h1 = min(H, h0 + q.seg);
+  char* rings = smem;
+  char* inb = smem + K::RING_BYTES;
+  float* bmb = reinterpret_cast<float*>(inb + K::IN_BYTES);   // [S-1][16*WCO]
+  float* bib = bmb + (S - 1) * 16 * WCO;
+  float* bma = bib + (S - 1) * 16 * WCO;                      // 1x1a BN [SW]
+  float* bia = bma + K::SW;
+  float* bmc = bia + K::SW;                                   // 1x1c BN [C]
+  float* bic = bmc + C;
+  const bf16_t* __restrict__ X = reinterpret_cast<const bf16_t*>(q.x);
+  bf16_t* __restrict__ Y = reinterpret_cast<bf16_t*>(q.y);
+  const size_t img = (size_t)n * H * W;
+
+  for (int i = tid; i < K::RING_BYTES / 16; i += NT)
+    reinterpret_cast<uint4*>(rings)[i] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+  for (int k = 0; k < S - 1; ++k)
+    for (int c = tid; c < 16 * WCO; c += NT) {
+      bmb[k * 16 * WCO + c] = c < WID ? q.mb[k][c] : 0.f;
+      bib[k * 16 * WCO + c] = c < WID ? q.ib[k][c] : 0.f;
+    }
+  for (int c = tid; c < K::SW; c += NT) { bma[c] = q.ma[c]; bia[c] = q.ia[c]; }
+  for (int c = tid; c < C; c += NT) { bmc[c] = q.mc[c]; bic[c] = q.ic[c]; }
+
+  // ---- per-wave constant operands
+  const bool is_a = wave < K::NPA;
+  const bool is_c = wave >= NW - K::NPC;
+  const int pq = is_a ? wave : wave - (NW - K::NPC);   // 1x1 pair of this wave
+  bf16x8 w1[K::KSW][2];
+  {
+    const bf16_t* __restrict__ Wp = reinterpret_cast<const bf16_t*>(is_a ? q.wa : q.wc);
+    const int kp = is_a ? C : K::SW;
+    const int ks = is_a ? K::KSA : K::KSC;
+#pragma unroll
+    for (int s = 0; s < K::KSW; ++s)
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+        w1[s][u] = ((is_a || is_c) && s < ks)
+                       ? ld16(Wp + (size_t)((2 * pq + u) * 16 + col) * kp + 32 * s + 8 * g)
+                       : bf16x8{};
+  }
+  // this lane's 8 BN channels of its 1x1 pair (LDS)
+  const float* bn1m = (is_a ? bma : bmc) + 32 * pq + 8 * g;
+  const float* bn1i = (is_a ? bia : bic) + 32 * pq + 8 * g;
+  const int ci = wave % WCO;                          // 3x3 cout tile of this wave
+  const bool chain_wave = wave < (NW / WCO) * WCO;
+  bf16x8 wb[S - 1][KST];
+#pragma unroll
+  for (int k = 0; k < S - 1; ++k) {
+    const bf16_t* __restrict__ Wk = reinterpret_cast<const bf16_t*>(q.wb[k]);
+#pragma unroll
+    for (int s = 0; s < KST; ++s) {
+      const int kk = 32 * s + 8 * g;
+      wb[k][s] = (chain_wave && kk < K::KFLAT)
+                     ? ld16(Wk + (size_t)(ci * 16 + col) * K::KFLAT + kk) : bf16x8{};
+    }
+  }
+  // k-step table of this lane group: tap row (0..2) << 24 | (byte offset + 2^15)
+  int ktab[KST];
+#pragma unroll
+  for (int s = 0; s < KST; ++s) {
+    const int kk = 32 * s + 8 * g;
+    int dyi = 1, off = 0;
+    if (kk < K::KFLAT) {
+      const int tap = kk / WID, ch = kk - tap * WID;
+      dyi = tap / 3;
+      off = (tap % 3 - 1) * ASTR + ch * 2;
+    }
+    ktab[s] = (dyi << 24) | (off + 32768);
+  }
+
+  // ---- input rows: global -> registers (prefetch) -> LDS
+  uint4 inr[K::IREG];
+  auto load_in = [&](int r) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < K::IREG; ++i) {
+      const int c = tid + i * NT;
+      const int px = c / K::CU, u = c - px * K::CU;
+      inr[i] = make_uint4(0, 0, 0, 0);
+      if (c < 16 * PT * K::CU && px < W && r >= 0 && r < H)
+        inr[i] = *reinterpret_cast<const uint4*>(X + (img + (size_t)r * W + px) * C + u * 8);
+    }
+  };
+  auto store_in = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < K::IREG; ++i) {
+      const int c = tid + i * NT;
+      const int px = c / K::CU, u = c - px * K::CU;
+      if (c < 16 * PT * K::CU) *reinterpret_cast<uint4*>(inb + px * K::ISTR + u * 16) = inr[i];
+    }
+  };
+  bf16x8 res[PT];
+  auto load_res = [&](int r) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < PT; ++j) {
+      const int px = 16 * j + col;
+      res[j] = (is_c && r >= h0 && r < h1 && px < W)
+                   ? ld16(X + (img + (size_t)r * W + px) * C + 32 * pq + 8 * g) : bf16x8{};
+    }
+  };
+
+  const int a0 = h0 - (S - 1);
+  const int steps = (h1 - h0) + 2 * S - 1;
+  load_in(a0);
+  store_in();
+  load_res(a0 - S);
+  __syncthreads();
+
+  for (int t = 0; t < steps; ++t) {
+    const int a = a0 + t;
+    const int c = a - S;
+    load_in(a + 1);  // lands during this step, goes to LDS in phase 1
+    // ---------------- phase 0: 1x1a (row a) | 1x1c (row c)
+    if (is_a) {
+      const bool inimg = a >= 0 && a < H;
+      const int ch = 32 * pq + 8 * g;
+      const int p = ch / WID, off = ch - p * WID;
+      char* dst;
+      if (p == 0) dst = rings + (K::ZB(1) + slot<3>(a)) * ROWB;
+      else if (p == S - 1) dst = rings + (K::XB(S) + slot<S + 1>(a)) * ROWB;
+      else {
+        // x_{p+1}, depth p+1 (p = 1..S-2)
+        int sl = 0;
+#pragma unroll
+        for (int d = 2; d < S; ++d)
+          if (p + 1 == d) sl = K::XB(d) + (a + 840) % d;
+        dst = rings + sl * ROWB;
+      }
+      dst += off * 2;
+#pragma unroll
+      for (int j = 0; j < PT; ++j) {
+        const int px = 16 * j + col;
+        bf16x8 b[K::KSA];
+#pragma unroll
+        for (int s = 0; s < K::KSA; ++s)
+          b[s] = *reinterpret_cast<const bf16x8*>(inb + px * K::ISTR + (32 * s + 8 * g) * 2);
+        f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < K::KSA; ++s) {
+          acc0 = mfma_step(w1[s][0], b[s], acc0);
+          acc1 = mfma_step(w1[s][1], b[s], acc1);
+        }
+        const f32x4 m0 = *reinterpret_cast<const f32x4*>(bn1m);
+        const f32x4 m1 = *reinterpret_cast<const f32x4*>(bn1m + 4);
+        const f32x4 i0 = *reinterpret_cast<const f32x4*>(bn1i);
+        const f32x4 i1 = *reinterpret_cast<const f32x4*>(bn1i + 4);
+        bf16x8 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          o[e] = (bf16_t)fmaxf((acc0[e] - m0[e]) * i0[e], 0.f);
+          o[4 + e] = (bf16_t)fmaxf((acc1[e] - m1[e]) * i1[e], 0.f);
+        }
+        if (!inimg) o = bf16x8{};
+        if (px < W) *reinterpret_cast<bf16x8*>(dst + (px + 1) * ASTR) = o;
+        __builtin_amdgcn_sched_barrier(0);  // one pixel tile in flight (register budget)
+      }
+    } else if (is_c && c >= h0 && c < h1) {
+      // B chunk s of lane group g: concat channel 32s+8g -> (plane, offset)
+      const char* src[K::KSC];
+#pragma unroll
+      for (int s = 0; s < K::KSC; ++s) {
+        const int ch = 32 * s + 8 * g;
+        const int p = ch / WID, off = ch - p * WID;
+        int sl = K::XB(S) + slot<S + 1>(c);
+#pragma unroll
+        for (int d = 1; d < S; ++d)
+          if (p + 1 == d) sl = K::YB(d) + (c + 840) % (S - d);
+        src[s] = rings + sl * ROWB + off * 2;
+      }
+      const int ch = 32 * pq + 8 * g;
+#pragma unroll
+      for (int j = 0; j < PT; ++j) {
+        const int px = 16 * j + col;
+        bf16x8 b[K::KSC];
+#pragma unroll
+        for (int s = 0; s < K::KSC; ++s)
+          b[s] = *reinterpret_cast<const bf16x8*>(src[s] + (px + 1) * ASTR);
+        f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < K::KSC; ++s) {
+          acc0 = mfma_step(w1[s][0], b[s], acc0);
+          acc1 = mfma_step(w1[s][1], b[s], acc1);
+        }
+        const f32x4 m0 = *reinterpret_cast<const f32x4*>(bn1m);
+        const f32x4 m1 = *reinterpret_cast<const f32x4*>(bn1m + 4);
+        const f32x4 i0 = *reinterpret_cast<const f32x4*>(bn1i);
+        const f32x4 i1 = *reinterpret_cast<const f32x4*>(bn1i + 4);
+        bf16x8 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          // BN, then the residual add, each rounded like the unfused epilogue (no FMA)
+#pragma clang fp contract(off)
+          float v0 = (acc0[e] - m0[e]) * i0[e] + (float)res[j][e];
+          float v1 = (acc1[e] - m1[e]) * i1[e] + (float)res[j][4 + e];
+          o[e] = (bf16_t)fmaxf(v0, 0.f);
+          o[4 + e] = (bf16_t)fmaxf(v1, 0.f);
+        }
+        if (px < W)
+          *reinterpret_cast<bf16x8*>(Y + (img + (size_t)c * W + px) * C + ch) = o;
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    load_res(c + 1);
+    __syncthreads();
+    // ---------------- phases 1..S-1: 3x3 stage k on row a-k
+#pragma unroll
+    for (int k = 1; k < S; ++k) {
+      if (k == 1) store_in();
+      const int r = a - k;
+      const bool inimg = r >= 0 && r < H;
+      const char* zb = rings + K::ZB(k) * ROWB;
+      const int rb0 = slot<3>(r - 1) * ROWB, rb1 = slot<3>(r) * ROWB, rb2 = slot<3>(r + 1) * ROWB;
+      const int co = 16 * ci + 4 * g;
+      char* ydst = rings + (K::YB(k) + (r + 840) % (S - k)) * ROWB + co * 2;
+      char* zdst = nullptr;
+      const char* xsrc = nullptr;
+      if (k < S - 1) {
+        zdst = rings + (K::ZB(k + 1) + slot<3>(r)) * ROWB + co * 2;
+        xsrc = rings + (K::XB(k + 1) + (r + 840) % (k + 1)) * ROWB + co * 2;
+      }
+      const float* bm = bmb + (k - 1) * 16 * WCO + co;
+      const float* bi = bib + (k - 1) * 16 * WCO + co;
+      if (chain_wave) {
+        for (int j = wave / WCO; j < PT; j += NW / WCO) {
+          const int px = 16 * j + col;
+          const bool st = co < WID && px < W;
+          if (!inimg) {
+            if (zdst && st) *reinterpret_cast<bf16x4*>(zdst + (px + 1) * ASTR) = bf16x4{};
+            continue;
+          }
+          f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+          const char* pb = zb + (px + 1) * ASTR - 32768;
+          bf16x8 bb[KST];
+#pragma unroll
+          for (int s = 0; s < KST; ++s) {
+            int e = ktab[s];
+            asm volatile("" : "+v"(e));  // keep the address math in the loop (no hoisting)
+            const int dyi = e >> 24;
+            const int rb = dyi == 0 ? rb0 : (dyi == 1 ? rb1 : rb2);
+            bb[s] = *reinterpret_cast<const bf16x8*>(pb + rb + (e & 0xFFFFFF));
+          }
+#pragma unroll
+          for (int s = 0; s < KST; ++s) acc = mfma_step(wb[k - 1][s], bb[s], acc);
+          if (st) {
+            const f32x4 m = *reinterpret_cast<const f32x4*>(bm);
+            const f32x4 sc = *reinterpret_cast<const f32x4*>(bi);
+            bf16x4 y;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) y[e] = (bf16_t)fmaxf((acc[e] - m[e]) * sc[e], 0.f);
+            *reinterpret_cast<bf16x4*>(ydst + (px + 1) * ASTR) = y;
+            if (zdst) {
+              const bf16x4 x = *reinterpret_cast<const bf16x4*>(xsrc + (px + 1) * ASTR);
+              *reinterpret_cast<bf16x4*>(zdst + (px + 1) * ASTR) = add4(x, y);
+            }
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+template <int C, int WID, int S, int PT>
+static hipError_t launch_bneck_t(const BneckParams& q, hipStream_t s) {
+  using K = BneckCfg<C, WID, S, PT>;
+  hipLaunchKernelGGL((bneck_fused<C, WID, S, PT>), dim3(q.N * q.nseg), dim3(512), K::LDS, s, q);
+  return hipGetLastError();
+}
+
+// Instantiated shapes: (C, w, split, pixel tiles of the frequency axis).
+#define BNECK_SHAPES(X) \
+  X(128, 24, 4, 5)      /* res2net50_w24_s4_c32, layer 1 at 80-d features */ \
+  X(128, 24, 4, 3)      /* ... at 40-d features */
+
+int bneck_lds(int C, int wid, int s, int W) {
+  const int pt = (W + 15) / 16;
+#define X_LDS(c_, w_, s_, p_) \
+  if (C == c_ && wid == w_ && s == s_ && pt == p_) return BneckCfg<c_, w_, s_, p_>::LDS;
+  BNECK_SHAPES(X_LDS)
+#undef X_LDS
+  return -1;
+}
+
+hipError_t launch_bneck(const BneckParams& q, int C, int wid, int s, hipStream_t st) {
+  const int pt = (q.W + 15) / 16;
+#define X_LAUNCH(c_, w_, s_, p_) \
+  if (C == c_ && wid == w_ && s == s_ && pt == p_) return launch_bneck_t<c_, w_, s_, p_>(q, st);
+  BNECK_SHAPES(X_LAUNCH)
+#undef X_LAUNCH
+  return hipErrorInvalidValue;
+}
+
+}  // namespace vox

@@ -61,6 +61,24 @@ struct ChainParams {
 };
 hipError_t launch_split_chain(const ChainParams& q, int wco, int wpx, hipStream_t s);
 
+// Fused Res2Net identity bottleneck (stride 1): 1x1a + split chain + 1x1c +
+// residual in one launch, intermediates in LDS ring buffers (bneck.hip).
+// One workgroup per (utterance, segment of `seg` rows); blocks = N * nseg.
+struct BneckParams {
+  const void* x;                    // block input / residual [N][H][W][C] bf16
+  void* y;                          // block output [N][H][W][C]
+  int N, H, W, seg, nseg;
+  const void* wa;                   // 1x1a paired-row weights [split*w][C]
+  const float* ma; const float* ia;
+  const void* wb[8];                // 3x3 stage k [coutp][9*w] (tap-major)
+  const float* mb[8]; const float* ib[8];
+  const void* wc;                   // 1x1c paired-row weights [C][split*w]
+  const float* mc; const float* ic;
+};
+// LDS bytes of the instantiated shape, or -1 when (C, w, split, W) has none.
+int bneck_lds(int C, int w, int split, int W);
+hipError_t launch_bneck(const BneckParams& q, int C, int w, int split, hipStream_t s);
+
 // Stride-1 bf16 conv with the input window staged in LDS (weights in the
 // [coutp][taps*Cin] layout).
 hipError_t launch_conv_win(const ConvParams& p, const ConvLaunch& l, hipStream_t s);

@@ -14,13 +14,9 @@
 //  * avgpool3s2   -- AvgPool 3x3/2 VALID over the fixed-padded tensor, divisor 9
 //                    (res2net_model.py:27-28,77).
 #include "kernels.h"
+#include "device_common.h"
 
 namespace vox {
-
-typedef __bf16 bf16_t;
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 template <typename T> struct Tr;
 template <> struct Tr<bf16_t> {
@@ -33,25 +29,6 @@ template <> struct Tr<float> {
   static constexpr int KSTEP = 16;  // 4 x mfma 16x16x4 over a permuted K
   typedef f32x4 frag;
 };
-
-__device__ __forceinline__ bf16x8 ld16(const bf16_t* p) {
-  uint4 u = *reinterpret_cast<const uint4*>(p);
-  return __builtin_bit_cast(bf16x8, u);
-}
-__device__ __forceinline__ f32x4 ld16(const float* p) {
-  return *reinterpret_cast<const f32x4*>(p);
-}
-
-template <typename F> __device__ __forceinline__ F zero_frag() { return F{}; }
-
-// Elementwise helpers on fragments (in fp32).
-__device__ __forceinline__ bf16x8 frag_add(bf16x8 a, bf16x8 b) {
-  bf16x8 r;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) r[e] = (bf16_t)((float)a[e] + (float)b[e]);
-  return r;
-}
-__device__ __forceinline__ f32x4 frag_add(f32x4 a, f32x4 b) { return a + b; }
 
 __device__ __forceinline__ bf16x8 frag_bnrelu(bf16x8 a, const float* m, const float* iv) {
   bf16x8 r;
@@ -66,9 +43,6 @@ __device__ __forceinline__ f32x4 frag_bnrelu(f32x4 a, const float* m, const floa
   return r;
 }
 
-__device__ __forceinline__ f32x4 mfma_step(bf16x8 a, bf16x8 b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-}
 // f32: lane l holds k = 4*(l>>4)+j in element j of both operands; MFMA j uses
 // element j, i.e. internal k index kk <-> real k = 4*kk + j for A and B alike.
 __device__ __forceinline__ f32x4 mfma_step(f32x4 a, f32x4 b, f32x4 c) {
