@@ -218,10 +218,12 @@ struct vox_model {
   int win_cin = 0;             // VOXEMB_WIN_CIN=c: conv_win only for Cin == c (debug)
   bool no_rr = false;          // VOXEMB_NO_RR=1: disable conv1x1_rr
   bool no_gemm = false;        // VOXEMB_NO_GEMM=1: disable gemm1x1_lds
+  int gemm_min_k = 192;        // VOXEMB_GEMM_MIN_K: smallest K routed to gemm1x1_lds (K=128 is faster on rr)
   bool no_chain = false;       // VOXEMB_NO_CHAIN=1: unfused Res2Net branches
   bool no_stem = false;        // VOXEMB_NO_STEM=1: stem through the generic conv
   bool no_bneck = false;       // VOXEMB_NO_BNECK=1: unfused identity bottlenecks
   int bneck_nseg = 0;          // VOXEMB_BNECK_NSEG: force row segments per utterance (tests)
+  int bneck_dbg = 0;           // VOXEMB_BNECK_DBG: timing experiments (skips work; wrong results)
   int chain_r = 0, chain_wpx = 0, chain_nw = 0;  // VOXEMB_CHAIN_R / VOXEMB_CHAIN_WPX (tuning)
   int rr_wpx = 0, rr_wco = 0;  // VOXEMB_RR_WPX / VOXEMB_RR_WCO: tile overrides (tuning)
 };
@@ -272,8 +274,10 @@ static int make_conv(vox_model* m, const HostTensor& k, int groups, const HostTe
     HIPCHK(hipMemcpy(out.w->p, w.data(), w.size() * 4, hipMemcpyHostToDevice));
   }
   if (dt == BF16 && groups == 1 && taps == 1 && out.vec && out.coutp % 32 == 0) {
-    // paired rows: row (2q+u)*16 + 4g + e <- channel 32q + 8g + 4u + e
-    std::vector<uint16_t> h((size_t)out.coutp * out.kp, 0);
+    // paired rows: row (2q+u)*16 + 4g + e <- channel 32q + 8g + 4u + e;
+    // rows padded with zeros to a multiple of 128 (gemm1x1_lds cout tiles)
+    const int rows = (out.coutp + 127) / 128 * 128;
+    std::vector<uint16_t> h((size_t)rows * out.kp, 0);
     for (int row = 0; row < out.coutp; ++row) {
       const int q = row / 32, u = (row / 16) & 1, g = (row & 15) / 4, e = row & 3;
       const int co = 32 * q + 8 * g + 4 * u + e;
@@ -522,10 +526,14 @@ static void emit_conv(Builder& B, const ConvW& cw, Act x, const void* x2, int ld
     int ys = 1;
     while (gx * ys < 1024 && tiles / (ys * 2) >= op.cl.wco) ys *= 2;
     op.cl.splitk = ys;
-    // compute-bound shapes: LDS-tiled 128x128 GEMM
-    if (!B.m->no_gemm && !in_mean && cw.cinp % 64 == 0 && cw.cinp >= 256 && cw.coutp % 128 == 0 &&
-        cw.cout >= 256)
+    // compute-bound shapes: LDS-tiled 128x128 GEMM (cout padded to 128-row
+    // tiles with zero weights when that wastes at most a third of the tile)
+    const int cout128 = (cw.cout + 127) / 128 * 128;
+    if (!B.m->no_gemm && !in_mean && cw.cinp % 64 == 0 && cw.cinp >= B.m->gemm_min_k &&
+        cw.cout >= 128 && 3 * (cout128 - cw.cout) <= cout128) {
       op.type = 9;
+      p.coutp = cout128;
+    }
   }
   // bf16 convs (stride 1 or 2) without prologue: window-staged LDS kernel if
   // some (pixel tile, cout tile, channel chunk) fits the LDS budget
@@ -749,6 +757,7 @@ static int build_res2net(Builder& B, const float* x, int n, int t, float* out) {
             q.wb[j] = br.wtc->p; q.mb[j] = (const float*)br.mean->p; q.ib[j] = (const float*)br.inv->p;
           }
           q.wc = c1c.wpair->p; q.mc = (const float*)c1c.mean->p; q.ic = (const float*)c1c.inv->p;
+          q.dbg = m->bneck_dbg;
           Op op;
           op.kind = OP_CONV;
           op.type = 12;
@@ -1049,10 +1058,12 @@ extern "C" int vox_load_blob(const void* blob, size_t nbytes, int device, int pr
   if (const char* e = std::getenv("VOXEMB_NO_RR")) m->no_rr = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_RR_WPX")) m->rr_wpx = std::atoi(e);
   if (const char* e = std::getenv("VOXEMB_NO_GEMM")) m->no_gemm = std::atoi(e) != 0;
+  if (const char* e = std::getenv("VOXEMB_GEMM_MIN_K")) m->gemm_min_k = std::atoi(e);
   if (const char* e = std::getenv("VOXEMB_NO_CHAIN")) m->no_chain = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_NO_STEM")) m->no_stem = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_NO_BNECK")) m->no_bneck = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_BNECK_NSEG")) m->bneck_nseg = std::atoi(e);
+  if (const char* e = std::getenv("VOXEMB_BNECK_DBG")) m->bneck_dbg = std::atoi(e);
   if (const char* e = std::getenv("VOXEMB_CHAIN_R")) m->chain_r = std::atoi(e);
   if (const char* e = std::getenv("VOXEMB_CHAIN_WPX")) m->chain_wpx = std::atoi(e);
   if (const char* e = std::getenv("VOXEMB_CHAIN_NW")) m->chain_nw = std::atoi(e);

@@ -12,20 +12,23 @@
 // intermediate in LDS ring buffers, so HBM sees the block input once and the
 // block output once (~0.5 KB per pixel).
 //
-// Row pipeline, step t handles A-row a = h0-(S-1)+t:
-//   phase 0   : 1x1a on row a (input row staged in LDS)     -> rings x_1..x_S
-//               1x1c on row a-S (rings y_1..y_{S-1}, x_S)    -> HBM (+ residual)
-//   phase k   : 3x3 stage k on row a-k (ring z_k rows a-k-1..a-k+1)
-//               -> ring y_k, and z_{k+1} = x_{k+1} + y_k (bf16, as unfused)
-// Ring depths follow from the lags: z_k 3 rows, x_k k rows, x_S S+1 rows,
-// y_k S-k rows.  Rows outside the image are zero (SAME padding).  Segments
-// recompute 2(S-1) warm-up rows.
+// Row pipeline, two phases (one barrier each) per step; step t handles
+// A-row a = h0-(S-1)+t:
+//   phase 0 : 1x1a on row a (input row staged in LDS)       -> rings x_1..x_S
+//             1x1c on row a-2(S-1) (rings y_1..y_{S-1}, x_S) -> HBM (+ residual)
+//   phase 1 : every 3x3 stage k at once, on row a-2k+1 (ring z_k rows
+//             a-2k..a-2k+2, all written in earlier steps or phase 0)
+//             -> ring y_k, and z_{k+1} = x_{k+1} + y_k (bf16, as unfused)
+// Ring depths follow from the lags: z_1 3 rows, z_k 4, x_k 2k-2, x_S 2S-1,
+// y_k 2S-1-2k.  Rows outside the image are zero (SAME padding).  Segments
+// recompute 3(S-1) warm-up rows.
 //
 // Work split (8 waves): phase 0 -- waves 0..NPA-1 own one 32-channel pair of
 // 1x1a outputs, waves NW-NPC..NW-1 one pair of 1x1c outputs, each across all
 // pixel tiles, with that pair's weights held in registers for the whole
-// kernel; chain phases -- wave w owns cout tile w % WCO of every stage (its
-// weights in registers) and pixel tiles w/WCO, w/WCO + NW/WCO, ...
+// kernel; phase 1 -- wave w < (S-1)*WCO owns 3x3 stage w/WCO+1, cout tile
+// w % WCO (its weights in registers) across all pixel tiles, two pixel tiles'
+// MFMA chains interleaved.
 // Accumulation orders (K chunks of 32, paired-row 1x1 weights, flattened
 // tap-major 3x3 K) equal the unfused kernels', so results are bit-identical.
 #include "kernels.h"
@@ -50,13 +53,17 @@ struct BneckCfg {
   static constexpr int ISTR = IU * 16;                                // input-row pixel stride
   static constexpr int WR = 16 * PT + 2;  // ring row: pad | pixels | pad (+ tile slack)
   static constexpr int ROWB = WR * ASTR;
-  // ring planes (one image row each)
-  static constexpr int ZB(int k) { return 3 * (k - 1); }              // z_k, k = 1..S-1
-  static constexpr int ZEND = 3 * (S - 1);
-  static constexpr int XB(int k) { return ZEND + (k - 1) * k / 2 - 1; }  // x_k, k = 2..S
-  static constexpr int XEND = XB(S) + S + 1;
-  static constexpr int YB(int k) { return XEND + (k - 1) * S - (k - 1) * k / 2; }  // y_k
-  static constexpr int NPLANES = XEND + S * (S - 1) / 2;
+  // ring planes (one image row each) and depths
+  static constexpr int ZD(int k) { return k == 1 ? 3 : 4; }
+  static constexpr int ZB(int k) { return k == 1 ? 0 : 3 + 4 * (k - 2); }   // z_k, k = 1..S-1
+  static constexpr int ZEND = 3 + 4 * (S - 2);
+  static constexpr int XD(int k) { return k == S ? 2 * S - 1 : 2 * k - 2; }
+  static constexpr int XB(int k) { return ZEND + (k - 2) * (k - 1); }       // x_k, k = 2..S
+  static constexpr int XEND = XB(S) + 2 * S - 1;
+  static constexpr int YD(int k) { return 2 * S - 1 - 2 * k; }
+  static constexpr int YB(int k) { return XEND + (k - 1) * (2 * S - 1 - k); } // y_k, k = 1..S-1
+  static constexpr int NPLANES = XEND + (S - 1) * (S - 1);
+  static constexpr int LAG_C = 2 * (S - 1);  // 1x1c row = A row - LAG_C
   static constexpr int RING_BYTES = NPLANES * ROWB;
   static constexpr int IN_BYTES = 16 * PT * ISTR;
   static constexpr int BN_FLOATS = 2 * (S - 1) * 16 * WCO + 2 * SW + 2 * C;
@@ -130,17 +137,22 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
   // this lane's 8 BN channels of its 1x1 pair (LDS)
   const float* bn1m = (is_a ? bma : bmc) + 32 * pq + 8 * g;
   const float* bn1i = (is_a ? bia : bic) + 32 * pq + 8 * g;
-  const int ci = wave % WCO;                          // 3x3 cout tile of this wave
-  const bool chain_wave = wave < (NW / WCO) * WCO;
-  bf16x8 wb[S - 1][KST];
+  static_assert((S - 1) * WCO <= NW, "one (stage, cout tile) per wave");
+  const bool chain_wave = wave < (S - 1) * WCO;
+  const int ck = chain_wave ? wave / WCO + 1 : 1;     // 3x3 stage of this wave
+  const int ci = wave % WCO;                          // its cout tile
+  bf16x8 wb[KST];
+  {
+    const void* wk = q.wb[0];
 #pragma unroll
-  for (int k = 0; k < S - 1; ++k) {
-    const bf16_t* __restrict__ Wk = reinterpret_cast<const bf16_t*>(q.wb[k]);
+    for (int k = 1; k < S - 1; ++k)
+      if (ck == k + 1) wk = q.wb[k];
+    const bf16_t* __restrict__ Wk = reinterpret_cast<const bf16_t*>(wk);
 #pragma unroll
     for (int s = 0; s < KST; ++s) {
       const int kk = 32 * s + 8 * g;
-      wb[k][s] = (chain_wave && kk < K::KFLAT)
-                     ? ld16(Wk + (size_t)(ci * 16 + col) * K::KFLAT + kk) : bf16x8{};
+      wb[s] = (chain_wave && kk < K::KFLAT)
+                  ? ld16(Wk + (size_t)(ci * 16 + col) * K::KFLAT + kk) : bf16x8{};
     }
   }
   // k-step table of this lane group: tap row (0..2) << 24 | (byte offset + 2^15)
@@ -188,50 +200,31 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
   };
 
   const int a0 = h0 - (S - 1);
-  const int steps = (h1 - h0) + 2 * S - 1;
+  const int steps = (h1 - h0) + 3 * (S - 1);
   load_in(a0);
   store_in();
-  load_res(a0 - S);
+  load_res(a0 - K::LAG_C);
   __syncthreads();
 
   for (int t = 0; t < steps; ++t) {
     const int a = a0 + t;
-    const int c = a - S;
-    load_in(a + 1);  // lands during this step, goes to LDS in phase 1
+    const int c = a - K::LAG_C;
+    if (!(q.dbg & 8)) load_in(a + 1);  // lands during this step, goes to LDS in phase 1
     // ---------------- phase 0: 1x1a (row a) | 1x1c (row c)
-    if (is_a) {
+    if (is_a && !(q.dbg & 1)) {
       const bool inimg = a >= 0 && a < H;
       const int ch = 32 * pq + 8 * g;
       const int p = ch / WID, off = ch - p * WID;
-      char* dst;
-      if (p == 0) dst = rings + (K::ZB(1) + slot<3>(a)) * ROWB;
-      else if (p == S - 1) dst = rings + (K::XB(S) + slot<S + 1>(a)) * ROWB;
-      else {
-        // x_{p+1}, depth p+1 (p = 1..S-2)
-        int sl = 0;
+      int sl = K::ZB(1) + slot<3>(a);                // plane 0 -> z_1 = x_1
 #pragma unroll
-        for (int d = 2; d < S; ++d)
-          if (p + 1 == d) sl = K::XB(d) + (a + 840) % d;
-        dst = rings + sl * ROWB;
-      }
-      dst += off * 2;
-#pragma unroll
-      for (int j = 0; j < PT; ++j) {
-        const int px = 16 * j + col;
-        bf16x8 b[K::KSA];
-#pragma unroll
-        for (int s = 0; s < K::KSA; ++s)
-          b[s] = *reinterpret_cast<const bf16x8*>(inb + px * K::ISTR + (32 * s + 8 * g) * 2);
-        f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s = 0; s < K::KSA; ++s) {
-          acc0 = mfma_step(w1[s][0], b[s], acc0);
-          acc1 = mfma_step(w1[s][1], b[s], acc1);
-        }
-        const f32x4 m0 = *reinterpret_cast<const f32x4*>(bn1m);
-        const f32x4 m1 = *reinterpret_cast<const f32x4*>(bn1m + 4);
-        const f32x4 i0 = *reinterpret_cast<const f32x4*>(bn1i);
-        const f32x4 i1 = *reinterpret_cast<const f32x4*>(bn1i + 4);
+      for (int d = 2; d <= S; ++d)
+        if (p + 1 == d) sl = K::XB(d) + (a + 840) % K::XD(d);
+      char* dst = rings + sl * ROWB + off * 2;
+      const f32x4 m0 = *reinterpret_cast<const f32x4*>(bn1m);
+      const f32x4 m1 = *reinterpret_cast<const f32x4*>(bn1m + 4);
+      const f32x4 i0 = *reinterpret_cast<const f32x4*>(bn1i);
+      const f32x4 i1 = *reinterpret_cast<const f32x4*>(bn1i + 4);
+      auto epi = [&](const f32x4& acc0, const f32x4& acc1, int px) __attribute__((always_inline)) {
         bf16x8 o;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -240,111 +233,153 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
         }
         if (!inimg) o = bf16x8{};
         if (px < W) *reinterpret_cast<bf16x8*>(dst + (px + 1) * ASTR) = o;
-        __builtin_amdgcn_sched_barrier(0);  // one pixel tile in flight (register budget)
+      };
+#pragma unroll
+      for (int j = 0; j < PT; j += 2) {
+        const bool two = j + 1 < PT;
+        const int px = 16 * j + col;
+        bf16x8 b[K::KSA], bq[K::KSA];
+#pragma unroll
+        for (int s = 0; s < K::KSA; ++s) {
+          b[s] = *reinterpret_cast<const bf16x8*>(inb + px * K::ISTR + (32 * s + 8 * g) * 2);
+          bq[s] = two ? *reinterpret_cast<const bf16x8*>(inb + (px + 16) * K::ISTR + (32 * s + 8 * g) * 2)
+                      : bf16x8{};
+        }
+        f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, c0 = a0, c1 = a0;
+#pragma unroll
+        for (int s = 0; s < K::KSA; ++s) {
+          a0 = mfma_step(w1[s][0], b[s], a0);
+          a1 = mfma_step(w1[s][1], b[s], a1);
+          if (two) {
+            c0 = mfma_step(w1[s][0], bq[s], c0);
+            c1 = mfma_step(w1[s][1], bq[s], c1);
+          }
+        }
+        epi(a0, a1, px);
+        if (two) epi(c0, c1, px + 16);
       }
-    } else if (is_c && c >= h0 && c < h1) {
+    } else if (is_c && c >= h0 && c < h1 && !(q.dbg & 2)) {
       // B chunk s of lane group g: concat channel 32s+8g -> (plane, offset)
       const char* src[K::KSC];
 #pragma unroll
       for (int s = 0; s < K::KSC; ++s) {
         const int ch = 32 * s + 8 * g;
         const int p = ch / WID, off = ch - p * WID;
-        int sl = K::XB(S) + slot<S + 1>(c);
+        int sl = K::XB(S) + (c + 840) % K::XD(S);
 #pragma unroll
         for (int d = 1; d < S; ++d)
-          if (p + 1 == d) sl = K::YB(d) + (c + 840) % (S - d);
+          if (p + 1 == d) sl = K::YB(d) + (c + 840) % K::YD(d);
         src[s] = rings + sl * ROWB + off * 2;
       }
       const int ch = 32 * pq + 8 * g;
-#pragma unroll
-      for (int j = 0; j < PT; ++j) {
-        const int px = 16 * j + col;
-        bf16x8 b[K::KSC];
-#pragma unroll
-        for (int s = 0; s < K::KSC; ++s)
-          b[s] = *reinterpret_cast<const bf16x8*>(src[s] + (px + 1) * ASTR);
-        f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s = 0; s < K::KSC; ++s) {
-          acc0 = mfma_step(w1[s][0], b[s], acc0);
-          acc1 = mfma_step(w1[s][1], b[s], acc1);
-        }
-        const f32x4 m0 = *reinterpret_cast<const f32x4*>(bn1m);
-        const f32x4 m1 = *reinterpret_cast<const f32x4*>(bn1m + 4);
-        const f32x4 i0 = *reinterpret_cast<const f32x4*>(bn1i);
-        const f32x4 i1 = *reinterpret_cast<const f32x4*>(bn1i + 4);
+      const f32x4 m0 = *reinterpret_cast<const f32x4*>(bn1m);
+      const f32x4 m1 = *reinterpret_cast<const f32x4*>(bn1m + 4);
+      const f32x4 i0 = *reinterpret_cast<const f32x4*>(bn1i);
+      const f32x4 i1 = *reinterpret_cast<const f32x4*>(bn1i + 4);
+      auto epi = [&](const f32x4& acc0, const f32x4& acc1, const bf16x8& rv, int px)
+                     __attribute__((always_inline)) {
         bf16x8 o;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           // BN, then the residual add, each rounded like the unfused epilogue (no FMA)
 #pragma clang fp contract(off)
-          float v0 = (acc0[e] - m0[e]) * i0[e] + (float)res[j][e];
-          float v1 = (acc1[e] - m1[e]) * i1[e] + (float)res[j][4 + e];
+          float v0 = (acc0[e] - m0[e]) * i0[e] + (float)rv[e];
+          float v1 = (acc1[e] - m1[e]) * i1[e] + (float)rv[4 + e];
           o[e] = (bf16_t)fmaxf(v0, 0.f);
           o[4 + e] = (bf16_t)fmaxf(v1, 0.f);
         }
-        if (px < W)
-          *reinterpret_cast<bf16x8*>(Y + (img + (size_t)c * W + px) * C + ch) = o;
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-    load_res(c + 1);
-    __syncthreads();
-    // ---------------- phases 1..S-1: 3x3 stage k on row a-k
+        if (px < W) *reinterpret_cast<bf16x8*>(Y + (img + (size_t)c * W + px) * C + ch) = o;
+      };
 #pragma unroll
-    for (int k = 1; k < S; ++k) {
-      if (k == 1) store_in();
-      const int r = a - k;
-      const bool inimg = r >= 0 && r < H;
-      const char* zb = rings + K::ZB(k) * ROWB;
-      const int rb0 = slot<3>(r - 1) * ROWB, rb1 = slot<3>(r) * ROWB, rb2 = slot<3>(r + 1) * ROWB;
-      const int co = 16 * ci + 4 * g;
-      char* ydst = rings + (K::YB(k) + (r + 840) % (S - k)) * ROWB + co * 2;
-      char* zdst = nullptr;
-      const char* xsrc = nullptr;
-      if (k < S - 1) {
-        zdst = rings + (K::ZB(k + 1) + slot<3>(r)) * ROWB + co * 2;
-        xsrc = rings + (K::XB(k + 1) + (r + 840) % (k + 1)) * ROWB + co * 2;
-      }
-      const float* bm = bmb + (k - 1) * 16 * WCO + co;
-      const float* bi = bib + (k - 1) * 16 * WCO + co;
-      if (chain_wave) {
-        for (int j = wave / WCO; j < PT; j += NW / WCO) {
-          const int px = 16 * j + col;
-          const bool st = co < WID && px < W;
-          if (!inimg) {
-            if (zdst && st) *reinterpret_cast<bf16x4*>(zdst + (px + 1) * ASTR) = bf16x4{};
-            continue;
-          }
-          f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-          const char* pb = zb + (px + 1) * ASTR - 32768;
-          bf16x8 bb[KST];
+      for (int j = 0; j < PT; j += 2) {
+        const bool two = j + 1 < PT;
+        const int px = 16 * j + col;
+        bf16x8 b[K::KSC], bq[K::KSC];
 #pragma unroll
-          for (int s = 0; s < KST; ++s) {
-            int e = ktab[s];
-            asm volatile("" : "+v"(e));  // keep the address math in the loop (no hoisting)
-            const int dyi = e >> 24;
-            const int rb = dyi == 0 ? rb0 : (dyi == 1 ? rb1 : rb2);
-            bb[s] = *reinterpret_cast<const bf16x8*>(pb + rb + (e & 0xFFFFFF));
-          }
+        for (int s = 0; s < K::KSC; ++s) {
+          b[s] = *reinterpret_cast<const bf16x8*>(src[s] + (px + 1) * ASTR);
+          bq[s] = two ? *reinterpret_cast<const bf16x8*>(src[s] + (px + 17) * ASTR) : bf16x8{};
+        }
+        f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, c0 = a0, c1 = a0;
 #pragma unroll
-          for (int s = 0; s < KST; ++s) acc = mfma_step(wb[k - 1][s], bb[s], acc);
-          if (st) {
-            const f32x4 m = *reinterpret_cast<const f32x4*>(bm);
-            const f32x4 sc = *reinterpret_cast<const f32x4*>(bi);
-            bf16x4 y;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) y[e] = (bf16_t)fmaxf((acc[e] - m[e]) * sc[e], 0.f);
-            *reinterpret_cast<bf16x4*>(ydst + (px + 1) * ASTR) = y;
-            if (zdst) {
-              const bf16x4 x = *reinterpret_cast<const bf16x4*>(xsrc + (px + 1) * ASTR);
-              *reinterpret_cast<bf16x4*>(zdst + (px + 1) * ASTR) = add4(x, y);
-            }
+        for (int s = 0; s < K::KSC; ++s) {
+          a0 = mfma_step(w1[s][0], b[s], a0);
+          a1 = mfma_step(w1[s][1], b[s], a1);
+          if (two) {
+            c0 = mfma_step(w1[s][0], bq[s], c0);
+            c1 = mfma_step(w1[s][1], bq[s], c1);
           }
         }
+        epi(a0, a1, res[j], px);
+        if (two) epi(c0, c1, res[(j + 1) < PT ? j + 1 : j], px + 16);
       }
-      __syncthreads();
     }
+    if (!(q.dbg & 8)) load_res(c + 1);
+    __syncthreads();
+    // ---------------- phase 1: all 3x3 stages, stage k on row a-2k+1
+    if (!(q.dbg & 8)) store_in();
+    if (chain_wave && !(q.dbg & 4)) {
+      const int k = ck;
+      const int co = 16 * ci + 4 * g;
+      const int r = a - 2 * k + 1;
+      const bool inimg = r >= 0 && r < H;
+      // ring geometry of stage k (wave-uniform -> scalar registers)
+      const int zd = k == 1 ? 3 : 4;
+      const int zbase = k == 1 ? 0 : 3 + 4 * (k - 2);
+      const int rb0 = __builtin_amdgcn_readfirstlane((zbase + (r - 1 + 840) % zd) * ROWB);
+      const int rb1 = __builtin_amdgcn_readfirstlane((zbase + (r + 840) % zd) * ROWB);
+      const int rb2 = __builtin_amdgcn_readfirstlane((zbase + (r + 1 + 840) % zd) * ROWB);
+      const int ysl = __builtin_amdgcn_readfirstlane(
+          (K::XEND + (k - 1) * (2 * S - 1 - k) + (r + 840) % (2 * S - 1 - 2 * k)) * ROWB);
+      const bool chain_next = k < S - 1;
+      const int zsl = __builtin_amdgcn_readfirstlane((3 + 4 * (k - 1) + (r + 840) % 4) * ROWB);
+      const int xsl = __builtin_amdgcn_readfirstlane(
+          (K::ZEND + (k - 1) * k + (r + 840) % (2 * k)) * ROWB);
+      const f32x4 m = *reinterpret_cast<const f32x4*>(bmb + (k - 1) * 16 * WCO + co);
+      const f32x4 sc = *reinterpret_cast<const f32x4*>(bib + (k - 1) * 16 * WCO + co);
+      // per-lane B offsets of the k-steps for the three tap rows
+      int boff[KST];
+#pragma unroll
+      for (int s = 0; s < KST; ++s) {
+        int e = ktab[s];
+        asm volatile("" : "+v"(e));  // keep the select in the loop body (no hoisting)
+        const int dyi = e >> 24;
+        boff[s] = (dyi == 0 ? rb0 : (dyi == 1 ? rb1 : rb2)) + (e & 0xFFFFFF) - 32768 + ASTR;
+      }
+      auto epilogue = [&](const f32x4& acc, int px) __attribute__((always_inline)) {
+        if (!(co < WID && px < W)) return;
+        const int pxo = px * ASTR + co * 2 + ASTR;
+        bf16x4 y;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) y[e] = (bf16_t)fmaxf((acc[e] - m[e]) * sc[e], 0.f);
+        if (!inimg) y = bf16x4{};
+        *reinterpret_cast<bf16x4*>(rings + ysl + pxo) = y;
+        if (chain_next) {
+          const bf16x4 x = *reinterpret_cast<const bf16x4*>(rings + xsl + pxo);
+          // SAME padding of the next stage: z_{k+1} = 0 outside the image
+          *reinterpret_cast<bf16x4*>(rings + zsl + pxo) = inimg ? add4(x, y) : bf16x4{};
+        }
+      };
+      for (int j = 0; j < PT; j += 2) {
+        const bool two = j + 1 < PT;
+        const int px0 = 16 * j + col, px1 = px0 + 16;
+        bf16x8 b0[KST], b1[KST];
+#pragma unroll
+        for (int s = 0; s < KST; ++s) {
+          b0[s] = *reinterpret_cast<const bf16x8*>(rings + boff[s] + px0 * ASTR);
+          b1[s] = two ? *reinterpret_cast<const bf16x8*>(rings + boff[s] + px1 * ASTR) : bf16x8{};
+        }
+        f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < KST; ++s) {
+          acc0 = mfma_step(wb[s], b0[s], acc0);
+          acc1 = mfma_step(wb[s], b1[s], acc1);
+        }
+        epilogue(acc0, px0);
+        if (two) epilogue(acc1, px1);
+      }
+    }
+    __syncthreads();
   }
 }
 

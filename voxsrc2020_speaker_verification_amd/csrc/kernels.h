@@ -74,6 +74,7 @@ struct BneckParams {
   const float* mb[8]; const float* ib[8];
   const void* wc;                   // 1x1c paired-row weights [C][split*w]
   const float* mc; const float* ic;
+  int dbg;                          // timing experiments only: skip parts (0 = normal)
 };
 // LDS bytes of the instantiated shape, or -1 when (C, w, split, W) has none.
 int bneck_lds(int C, int w, int split, int W);
