@@ -1,6 +1,7 @@
 """The fused Res2Net bottleneck kernel (bneck.hip) on random data against a
 numpy emulation of the unfused block with the same bf16 rounding points
-(1x1a -> x, z_k = x_k + y_{k-1}, y_k, 1x1c + residual).  fp32 accumulation
+(1x1a -> x, z_k = x_k + y_{k-1}, y_k, 1x1c + identity or bf16 projection
+shortcut).  fp32 accumulation
 order differs between numpy and MFMA, so a small fraction of outputs may sit
 a few bf16 ulps apart; 99% are exact.  Called through the internal
 launcher (C++ symbol) with the host-side weight layouts of api.cpp.
@@ -25,7 +26,8 @@ class BneckParams(C.Structure):
                 ("N", C.c_int), ("H", C.c_int), ("W", C.c_int), ("seg", C.c_int), ("nseg", C.c_int),
                 ("wa", C.c_void_p), ("ma", C.c_void_p), ("ia", C.c_void_p),
                 ("wb", C.c_void_p * 8), ("mb", C.c_void_p * 8), ("ib", C.c_void_p * 8),
-                ("wc", C.c_void_p), ("mc", C.c_void_p), ("ic", C.c_void_p)]
+                ("wc", C.c_void_p), ("mc", C.c_void_p), ("ic", C.c_void_p),
+                ("wp", C.c_void_p), ("mp", C.c_void_p), ("ip", C.c_void_p), ("dbg", C.c_int)]
 
 
 def paired(wio):
@@ -49,14 +51,17 @@ def conv3x3_same(x, k):   # x [H][W][ci], k [3][3][ci][co]
 
 
 
-def _block(N, H, W, nseg, seed):
+def _block(N, H, W, nseg, seed, Ci=128):
     import torch
     from voxsrc2020_speaker_verification_amd import _native
     Cc, w, S = 128, 24, 4
     SW = S * w
     rng = np.random.default_rng(seed)
-    X = bf16(rng.standard_normal((N, H, W, Cc)))
-    Wa = bf16(rng.standard_normal((Cc, SW)) / np.sqrt(Cc))
+    X = bf16(rng.standard_normal((N, H, W, Ci)))
+    Wa = bf16(rng.standard_normal((Ci, SW)) / np.sqrt(Ci))
+    Wp = bf16(rng.standard_normal((Ci, Cc)) / np.sqrt(Ci))
+    mp = rng.standard_normal(Cc).astype(np.float32) * 0.1
+    ip = (1 + rng.random(Cc)).astype(np.float32)
     Wb = [bf16(rng.standard_normal((3, 3, w, w)) / np.sqrt(9 * w)) for _ in range(S - 1)]
     Wc = bf16(rng.standard_normal((SW, Cc)) / np.sqrt(SW))
     ma = rng.standard_normal(SW).astype(np.float32) * 0.1
@@ -75,12 +80,13 @@ def _block(N, H, W, nseg, seed):
             prev = bf16(np.maximum((conv3x3_same(z, Wb[k]) - mb[k]) * ib[k], 0))
             ys.append(prev)
         cat = np.concatenate(ys + [x[..., (S - 1) * w:]], -1)
-        refs.append(bf16(np.maximum((cat @ Wc - mc) * ic + X[i], 0)))
+        sc = X[i] if Ci == Cc else bf16((X[i] @ Wp - mp) * ip)   # identity / projection
+        refs.append(bf16(np.maximum((cat @ Wc - mc) * ic + sc, 0)))
     ref = np.stack(refs)
     tb = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float32)).cuda().to(torch.bfloat16)
     tf = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float32)).cuda()
     xd = tb(X)
-    yd = torch.zeros_like(xd)
+    yd = torch.zeros((N, H, W, Cc), dtype=torch.bfloat16, device="cuda")
     wa_d, wc_d = tb(paired(Wa)), tb(paired(Wc))
     wb_d = []
     for k in range(S - 1):
@@ -90,6 +96,7 @@ def _block(N, H, W, nseg, seed):
                 h[co, t * w:(t + 1) * w] = Wb[k][t // 3, t % 3, :, co]
         wb_d.append(tb(h))
     keep = [tf(ma), tf(ia), tf(mc), tf(ic)] + [tf(a) for a in mb] + [tf(a) for a in ib]
+    wp_d, mp_d, ip_d = tb(paired(Wp)), tf(mp), tf(ip)
     q = BneckParams()
     q.x, q.y = xd.data_ptr(), yd.data_ptr()
     q.N, q.H, q.W = N, H, W
@@ -101,18 +108,21 @@ def _block(N, H, W, nseg, seed):
         q.mb[k] = keep[4 + k].data_ptr()
         q.ib[k] = keep[4 + S - 1 + k].data_ptr()
     q.wc, q.mc, q.ic = wc_d.data_ptr(), keep[2].data_ptr(), keep[3].data_ptr()
-    fn = getattr(_native.lib(), "_ZN3vox12launch_bneckERKNS_11BneckParamsEiiiP12ihipStream_t")
+    q.wp, q.mp, q.ip = wp_d.data_ptr(), mp_d.data_ptr(), ip_d.data_ptr()
+    q.dbg = 0
+    fn = getattr(_native.lib(), "_ZN3vox12launch_bneckERKNS_11BneckParamsEiiiiP12ihipStream_t")
     fn.restype = C.c_int
-    fn.argtypes = [C.POINTER(BneckParams), C.c_int, C.c_int, C.c_int, C.c_void_p]
-    assert fn(C.byref(q), Cc, w, S, None) == 0
+    fn.argtypes = [C.POINTER(BneckParams), C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]
+    assert fn(C.byref(q), Ci, Cc, w, S, None) == 0
     torch.cuda.synchronize()
     return yd.float().cpu().numpy(), ref
 
 
-@pytest.mark.parametrize("N,H,W,nseg", [(1, 40, 80, 1), (3, 200, 80, 1), (3, 200, 80, 8),
-                                        (2, 33, 40, 3)])
-def test_bneck_matches_emulation(N, H, W, nseg):
-    got, ref = _block(N, H, W, nseg, seed=N * 1000 + H)
+@pytest.mark.parametrize("N,H,W,nseg,Ci", [(1, 40, 80, 1, 128), (3, 200, 80, 1, 128),
+                                           (3, 200, 80, 8, 128), (2, 33, 40, 3, 128),
+                                           (2, 50, 80, 2, 32), (1, 21, 40, 1, 32)])
+def test_bneck_matches_emulation(N, H, W, nseg, Ci):
+    got, ref = _block(N, H, W, nseg, seed=N * 1000 + H, Ci=Ci)
     # an intermediate that rounds one ulp apart (numpy vs MFMA summation order)
     # moves a few outputs by about one intermediate ulp; an indexing bug moves
     # whole rows / channels by O(1)

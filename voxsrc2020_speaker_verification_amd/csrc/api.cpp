@@ -188,7 +188,8 @@ struct Op {
              Ho = 0, Wo = 0;
   int64_t count = 0;
   ChainParams ch{};
-  BneckParams bq{};  // type 12: C, w (cl.wco), split (S)
+  BneckParams bq{};  // type 12: Cin (cin), C, w (cl.wco), split (S)
+  int cin = 0;
   double flops = 0, bytes = 0;
 };
 
@@ -731,21 +732,30 @@ static int build_res2net(Builder& B, const float* x, int n, int t, float* out) {
     for (int b = 0; b < blocks[st]; ++b) {
       const int stride = b == 0 ? strides[st] : 1;
       const int Ho = (H + stride - 1) / stride, Wo = (W + stride - 1) / stride;
-      if (stride == 1 && b > 0 && m->dt == BF16 && !m->no_bneck && cur.ld == cur.C &&
-          bneck_lds(cur.C, w, s, W) > 0) {
-        // whole identity bottleneck in one launch (bneck.hip)
-        const ConvW& c1a = m->convs[ci];
-        const ConvW& c1c = m->convs[ci + s];
-        bool ok = s - 1 <= 8 && c1a.wpair && c1c.wpair && c1a.cin == cur.C && c1a.cout == sw &&
-                  c1c.cin == sw && c1c.cout == cur.C && c1a.mean && c1c.mean;
+      if (stride == 1 && m->dt == BF16 && !m->no_bneck && cur.ld == cur.C) {
+        // whole bottleneck in one launch (bneck.hip): identity shortcut, or the
+        // 1x1 projection of block 0 (stride 1 only)
+        const bool proj = b == 0;
+        const size_t base = ci + (proj ? 1 : 0);
+        const ConvW& c1a = m->convs[base];
+        const ConvW& c1c = m->convs[base + s];
+        const int C = c1c.cout;
+        bool ok = (proj ? cur.C != C : cur.C == C) && bneck_lds(cur.C, C, w, s, W) > 0 &&
+                  s - 1 <= 8 && c1a.wpair && c1c.wpair && c1a.cin == cur.C && c1a.cout == sw &&
+                  c1c.cin == sw && c1a.mean && c1c.mean;
         for (int j = 0; ok && j < s - 1; ++j)
-          ok = m->convs[ci + 1 + j].wtc != nullptr && m->convs[ci + 1 + j].coutp >= 16 * ((w + 15) / 16);
+          ok = m->convs[base + 1 + j].wtc != nullptr &&
+               m->convs[base + 1 + j].coutp >= 16 * ((w + 15) / 16);
+        if (ok && proj) {
+          const ConvW& pr = m->convs[ci];
+          ok = pr.wpair && pr.cin == cur.C && pr.cout == C && pr.mean;
+        }
         if (ok) {
           BneckParams q{};
-          void* yo = B.base(nxt_s, (size_t)n * H * W * cur.C * es);
+          void* yo = B.base(nxt_s, (size_t)n * H * W * C * es);
           q.x = cur.p; q.y = yo; q.N = n; q.H = H; q.W = W;
           // one workgroup per CU: split utterances into row segments until the
-          // grid covers the chip (segments keep >= 16 rows; 2(s-1) warm-up rows each)
+          // grid covers the chip (segments keep >= 16 rows; 3(s-1) warm-up rows each)
           int nseg = 1;
           while (n * nseg < 256 && H / (2 * nseg) >= 16) nseg *= 2;
           if (m->bneck_nseg > 0) nseg = std::min(m->bneck_nseg, H);
@@ -753,22 +763,27 @@ static int build_res2net(Builder& B, const float* x, int n, int t, float* out) {
           q.nseg = (H + q.seg - 1) / q.seg;
           q.wa = c1a.wpair->p; q.ma = (const float*)c1a.mean->p; q.ia = (const float*)c1a.inv->p;
           for (int j = 0; j < s - 1; ++j) {
-            const ConvW& br = m->convs[ci + 1 + j];
+            const ConvW& br = m->convs[base + 1 + j];
             q.wb[j] = br.wtc->p; q.mb[j] = (const float*)br.mean->p; q.ib[j] = (const float*)br.inv->p;
           }
           q.wc = c1c.wpair->p; q.mc = (const float*)c1c.mean->p; q.ic = (const float*)c1c.inv->p;
+          if (proj) {
+            const ConvW& pr = m->convs[ci];
+            q.wp = pr.wpair->p; q.mp = (const float*)pr.mean->p; q.ip = (const float*)pr.inv->p;
+          }
           q.dbg = m->bneck_dbg;
           Op op;
           op.kind = OP_CONV;
           op.type = 12;
           op.bq = q;
-          op.C = cur.C; op.cl.wco = w; op.S = s;
+          op.cin = cur.C; op.C = C; op.cl.wco = w; op.S = s;
           const double px = (double)n * H * W;
-          op.flops = 2.0 * px * ((double)cur.C * sw + (s - 1) * 9.0 * w * w + (double)sw * cur.C);
-          op.bytes = (double)es * px * cur.C * 2.0;
+          op.flops = 2.0 * px * ((double)cur.C * sw + (s - 1) * 9.0 * w * w + (double)sw * C +
+                                 (proj ? (double)cur.C * C : 0.0));
+          op.bytes = (double)es * px * (cur.C + C + (proj ? 0 : C));
           B.ops->push_back(op);
-          ci += s + 1;
-          cur = Act{yo, cur.C, n, H, W, cur.C};
+          ci = base + s + 1;
+          cur = Act{yo, C, n, H, W, C};
           std::swap(cur_s, nxt_s);
           continue;
         }
@@ -998,7 +1013,7 @@ static hipError_t run_op(vox_model* m, const Op& op, hipStream_t s) {
     case 8: return launch_conv1x1_rr(op.cp, op.cl, s);
     case 9: return launch_gemm1x1(op.cp, s);
     case 10: return launch_split_chain(op.ch, op.cl.wco, op.cl.wpx, s);
-    case 12: return launch_bneck(op.bq, op.C, op.cl.wco, op.S, s);
+    case 12: return launch_bneck(op.bq, op.cin, op.C, op.cl.wco, op.S, s);
     case 11:
       return launch_stem(m->dt, (const float*)op.src, op.N, op.H, op.W, op.part, op.C, op.mean,
                          op.inv, op.dst, s);
@@ -1228,8 +1243,9 @@ extern "C" int vox_plan_describe(vox_model* m, const float* d_x, int n, int t, i
                     p.Cout, p.kh, p.kw, p.sh, p.groups, p.flags, p.x2 ? 1 : 0, p.in_mean ? 1 : 0,
                     o.flops, o.bytes);
     else if (o.type == 12)
-      std::snprintf(line, sizeof(line), "bneck N=%d H=%d W=%d C=%d w=%d split=%d seg=%d nseg=%d flops=%.4g bytes=%.4g\n",
-                    o.bq.N, o.bq.H, o.bq.W, o.C, o.cl.wco, o.S, o.bq.seg, o.bq.nseg, o.flops, o.bytes);
+      std::snprintf(line, sizeof(line), "bneck N=%d H=%d W=%d Cin=%d C=%d w=%d split=%d seg=%d nseg=%d flops=%.4g bytes=%.4g\n",
+                    o.bq.N, o.bq.H, o.bq.W, o.cin, o.C, o.cl.wco, o.S, o.bq.seg, o.bq.nseg, o.flops,
+                    o.bytes);
     else if (o.type == 10)
       std::snprintf(line, sizeof(line), "chain wco=%d wpx=%d N=%d H=%d W=%d w=%d nst=%d R=%d lds=%d flops=%.4g bytes=%.4g\n",
                     o.cl.wco, o.cl.wpx, o.ch.N, o.ch.H, o.ch.W, o.ch.w, o.ch.nst, o.ch.R, o.ch.lds,

@@ -36,11 +36,13 @@
 
 namespace vox {
 
-template <int C, int WID, int S, int PT>
+template <int CI, int C, int WID, int S, int PT>
 struct BneckCfg {
   static constexpr int NW = 8, NT = 64 * NW;
+  static constexpr bool PROJ = CI != C;              // projection shortcut (block 0)
+  static constexpr int KSP = CI / 32;                // its k-steps
   static constexpr int SW = S * WID;
-  static constexpr int NPA = SW / 32, KSA = C / 32;  // 1x1a: output pairs, k-steps
+  static constexpr int NPA = SW / 32, KSA = CI / 32; // 1x1a: output pairs, k-steps
   static constexpr int NPC = C / 32, KSC = SW / 32;  // 1x1c
   static constexpr int KSW = KSA > KSC ? KSA : KSC;
   static constexpr int WCO = (WID + 15) / 16;        // 3x3 cout tiles
@@ -49,7 +51,7 @@ struct BneckCfg {
   static constexpr int KST = KCP / 32;
   static constexpr int AU = ((WID / 8) & 1) ? WID / 8 : WID / 8 + 1;  // odd 16-B units
   static constexpr int ASTR = AU * 16;                                // ring pixel stride
-  static constexpr int IU = ((C / 8) & 1) ? C / 8 : C / 8 + 1;
+  static constexpr int IU = ((CI / 8) & 1) ? CI / 8 : CI / 8 + 1;
   static constexpr int ISTR = IU * 16;                                // input-row pixel stride
   static constexpr int WR = 16 * PT + 2;  // ring row: pad | pixels | pad (+ tile slack)
   static constexpr int ROWB = WR * ASTR;
@@ -66,9 +68,9 @@ struct BneckCfg {
   static constexpr int LAG_C = 2 * (S - 1);  // 1x1c row = A row - LAG_C
   static constexpr int RING_BYTES = NPLANES * ROWB;
   static constexpr int IN_BYTES = 16 * PT * ISTR;
-  static constexpr int BN_FLOATS = 2 * (S - 1) * 16 * WCO + 2 * SW + 2 * C;
+  static constexpr int BN_FLOATS = 2 * (S - 1) * 16 * WCO + 2 * SW + 2 * C + (PROJ ? 2 * C : 0);
   static constexpr int LDS = RING_BYTES + IN_BYTES + 4 * BN_FLOATS;
-  static constexpr int CU = C / 8;                            // 16-B chunks per input pixel
+  static constexpr int CU = CI / 8;                           // 16-B chunks per input pixel
   static constexpr int IREG = (16 * PT * CU + NT - 1) / NT;   // input-row chunks per thread
 };
 
@@ -82,9 +84,10 @@ __device__ __forceinline__ bf16x4 add4(bf16x4 a, bf16x4 b) {
   return r;
 }
 
-template <int C, int WID, int S, int PT>
+template <int CI, int C, int WID, int S, int PT>
 __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
-  using K = BneckCfg<C, WID, S, PT>;
+  using K = BneckCfg<CI, C, WID, S, PT>;
+  static_assert(!K::PROJ || K::KSP == 1, "projection shortcut: one k-step (Cin 32)");
   constexpr int NW = K::NW, NT = K::NT, WCO = K::WCO, KST = K::KST;
   constexpr int ASTR = K::ASTR, ROWB = K::ROWB;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -102,6 +105,8 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
   float* bia = bma + K::SW;
   float* bmc = bia + K::SW;                                   // 1x1c BN [C]
   float* bic = bmc + C;
+  float* bmp = bic + C;                                       // projection BN [C]
+  float* bip = bmp + C;
   const bf16_t* __restrict__ X = reinterpret_cast<const bf16_t*>(q.x);
   bf16_t* __restrict__ Y = reinterpret_cast<bf16_t*>(q.y);
   const size_t img = (size_t)n * H * W;
@@ -116,6 +121,8 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
     }
   for (int c = tid; c < K::SW; c += NT) { bma[c] = q.ma[c]; bia[c] = q.ia[c]; }
   for (int c = tid; c < C; c += NT) { bmc[c] = q.mc[c]; bic[c] = q.ic[c]; }
+  if (K::PROJ)
+    for (int c = tid; c < C; c += NT) { bmp[c] = q.mp[c]; bip[c] = q.ip[c]; }
 
   // ---- per-wave constant operands
   const bool is_a = wave < K::NPA;
@@ -124,7 +131,7 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
   bf16x8 w1[K::KSW][2];
   {
     const bf16_t* __restrict__ Wp = reinterpret_cast<const bf16_t*>(is_a ? q.wa : q.wc);
-    const int kp = is_a ? C : K::SW;
+    const int kp = is_a ? CI : K::SW;
     const int ks = is_a ? K::KSA : K::KSC;
 #pragma unroll
     for (int s = 0; s < K::KSW; ++s)
@@ -137,6 +144,13 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
   // this lane's 8 BN channels of its 1x1 pair (LDS)
   const float* bn1m = (is_a ? bma : bmc) + 32 * pq + 8 * g;
   const float* bn1i = (is_a ? bia : bic) + 32 * pq + 8 * g;
+  // projection shortcut pair of a 1x1c wave (block 0): weights in registers
+  bf16x8 wp[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+    wp[u] = (K::PROJ && is_c)
+                ? ld16(reinterpret_cast<const bf16_t*>(q.wp) + (size_t)((2 * pq + u) * 16 + col) * CI + 8 * g)
+                : bf16x8{};
   static_assert((S - 1) * WCO <= NW, "one (stage, cout tile) per wave");
   const bool chain_wave = wave < (S - 1) * WCO;
   const int ck = chain_wave ? wave / WCO + 1 : 1;     // 3x3 stage of this wave
@@ -178,7 +192,7 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
       const int px = c / K::CU, u = c - px * K::CU;
       inr[i] = make_uint4(0, 0, 0, 0);
       if (c < 16 * PT * K::CU && px < W && r >= 0 && r < H)
-        inr[i] = *reinterpret_cast<const uint4*>(X + (img + (size_t)r * W + px) * C + u * 8);
+        inr[i] = *reinterpret_cast<const uint4*>(X + (img + (size_t)r * W + px) * CI + u * 8);
     }
   };
   auto store_in = [&]() __attribute__((always_inline)) {
@@ -194,8 +208,11 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
 #pragma unroll
     for (int j = 0; j < PT; ++j) {
       const int px = 16 * j + col;
+      // identity: this lane's 8 residual channels; projection: its B chunk of
+      // the (CI = 32)-channel input row, for the shortcut MFMAs
+      const int cho = K::PROJ ? 8 * g : 32 * pq + 8 * g;
       res[j] = (is_c && r >= h0 && r < h1 && px < W)
-                   ? ld16(X + (img + (size_t)r * W + px) * C + 32 * pq + 8 * g) : bf16x8{};
+                   ? ld16(X + (img + (size_t)r * W + px) * CI + cho) : bf16x8{};
     }
   };
 
@@ -276,8 +293,22 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
       const f32x4 m1 = *reinterpret_cast<const f32x4*>(bn1m + 4);
       const f32x4 i0 = *reinterpret_cast<const f32x4*>(bn1i);
       const f32x4 i1 = *reinterpret_cast<const f32x4*>(bn1i + 4);
-      auto epi = [&](const f32x4& acc0, const f32x4& acc1, const bf16x8& rv, int px)
+      auto epi = [&](const f32x4& acc0, const f32x4& acc1, bf16x8 rv, int px)
                      __attribute__((always_inline)) {
+        if (K::PROJ) {
+          // shortcut = bf16(bn_p(conv1x1_p(in))), as the unfused projection writes it
+          const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+          const f32x4 s0 = mfma_step(wp[0], rv, z), s1 = mfma_step(wp[1], rv, z);
+          const f32x4 pm0 = *reinterpret_cast<const f32x4*>(bmp + ch);
+          const f32x4 pm1 = *reinterpret_cast<const f32x4*>(bmp + ch + 4);
+          const f32x4 pi0 = *reinterpret_cast<const f32x4*>(bip + ch);
+          const f32x4 pi1 = *reinterpret_cast<const f32x4*>(bip + ch + 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            rv[e] = (bf16_t)((s0[e] - pm0[e]) * pi0[e]);
+            rv[4 + e] = (bf16_t)((s1[e] - pm1[e]) * pi1[e]);
+          }
+        }
         bf16x8 o;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -383,31 +414,35 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
   }
 }
 
-template <int C, int WID, int S, int PT>
+template <int CI, int C, int WID, int S, int PT>
 static hipError_t launch_bneck_t(const BneckParams& q, hipStream_t s) {
-  using K = BneckCfg<C, WID, S, PT>;
-  hipLaunchKernelGGL((bneck_fused<C, WID, S, PT>), dim3(q.N * q.nseg), dim3(512), K::LDS, s, q);
+  using K = BneckCfg<CI, C, WID, S, PT>;
+  hipLaunchKernelGGL((bneck_fused<CI, C, WID, S, PT>), dim3(q.N * q.nseg), dim3(512), K::LDS, s, q);
   return hipGetLastError();
 }
 
-// Instantiated shapes: (C, w, split, pixel tiles of the frequency axis).
+// Instantiated shapes: (Cin, C, w, split, pixel tiles of the frequency axis).
 #define BNECK_SHAPES(X) \
-  X(128, 24, 4, 5)      /* res2net50_w24_s4_c32, layer 1 at 80-d features */ \
-  X(128, 24, 4, 3)      /* ... at 40-d features */
+  X(128, 128, 24, 4, 5) /* res2net50_w24_s4_c32 layer 1, identity blocks, 80-d */ \
+  X(128, 128, 24, 4, 3) /* ... 40-d features */                                   \
+  X(32, 128, 24, 4, 5)  /* ... layer-1 block 0 (projection shortcut), 80-d */     \
+  X(32, 128, 24, 4, 3)  /* ... 40-d */
 
-int bneck_lds(int C, int wid, int s, int W) {
+int bneck_lds(int CI, int C, int wid, int s, int W) {
   const int pt = (W + 15) / 16;
-#define X_LDS(c_, w_, s_, p_) \
-  if (C == c_ && wid == w_ && s == s_ && pt == p_) return BneckCfg<c_, w_, s_, p_>::LDS;
+#define X_LDS(ci_, c_, w_, s_, p_)                                            \
+  if (CI == ci_ && C == c_ && wid == w_ && s == s_ && pt == p_)               \
+    return BneckCfg<ci_, c_, w_, s_, p_>::LDS;
   BNECK_SHAPES(X_LDS)
 #undef X_LDS
   return -1;
 }
 
-hipError_t launch_bneck(const BneckParams& q, int C, int wid, int s, hipStream_t st) {
+hipError_t launch_bneck(const BneckParams& q, int CI, int C, int wid, int s, hipStream_t st) {
   const int pt = (q.W + 15) / 16;
-#define X_LAUNCH(c_, w_, s_, p_) \
-  if (C == c_ && wid == w_ && s == s_ && pt == p_) return launch_bneck_t<c_, w_, s_, p_>(q, st);
+#define X_LAUNCH(ci_, c_, w_, s_, p_)                                         \
+  if (CI == ci_ && C == c_ && wid == w_ && s == s_ && pt == p_)               \
+    return launch_bneck_t<ci_, c_, w_, s_, p_>(q, st);
   BNECK_SHAPES(X_LAUNCH)
 #undef X_LAUNCH
   return hipErrorInvalidValue;

@@ -61,11 +61,12 @@ struct ChainParams {
 };
 hipError_t launch_split_chain(const ChainParams& q, int wco, int wpx, hipStream_t s);
 
-// Fused Res2Net identity bottleneck (stride 1): 1x1a + split chain + 1x1c +
-// residual in one launch, intermediates in LDS ring buffers (bneck.hip).
+// Fused Res2Net bottleneck (stride 1): 1x1a + split chain + 1x1c + identity
+// or 1x1-projection shortcut in one launch, intermediates in LDS ring
+// buffers (bneck.hip).
 // One workgroup per (utterance, segment of `seg` rows); blocks = N * nseg.
 struct BneckParams {
-  const void* x;                    // block input / residual [N][H][W][C] bf16
+  const void* x;                    // block input [N][H][W][Cin] bf16
   void* y;                          // block output [N][H][W][C]
   int N, H, W, seg, nseg;
   const void* wa;                   // 1x1a paired-row weights [split*w][C]
@@ -74,11 +75,13 @@ struct BneckParams {
   const float* mb[8]; const float* ib[8];
   const void* wc;                   // 1x1c paired-row weights [C][split*w]
   const float* mc; const float* ic;
+  const void* wp;                   // projection shortcut [C][Cin] paired rows (Cin != C)
+  const float* mp; const float* ip;
   int dbg;                          // timing experiments only: skip parts (0 = normal)
 };
 // LDS bytes of the instantiated shape, or -1 when (C, w, split, W) has none.
-int bneck_lds(int C, int w, int split, int W);
-hipError_t launch_bneck(const BneckParams& q, int C, int w, int split, hipStream_t s);
+int bneck_lds(int Cin, int C, int w, int split, int W);
+hipError_t launch_bneck(const BneckParams& q, int Cin, int C, int w, int split, hipStream_t s);
 
 // Stride-1 bf16 conv with the input window staged in LDS (weights in the
 // [coutp][taps*Cin] layout).
