@@ -223,6 +223,7 @@ struct vox_model {
   bool no_chain = false;       // VOXEMB_NO_CHAIN=1: unfused Res2Net branches
   bool no_stem = false;        // VOXEMB_NO_STEM=1: stem through the generic conv
   bool no_bneck = false;       // VOXEMB_NO_BNECK=1: unfused identity bottlenecks
+  bool no_chain_rows = false;  // VOXEMB_NO_CHAIN_ROWS=1: row-tiled split_chain instead
   int bneck_nseg = 0;          // VOXEMB_BNECK_NSEG: force row segments per utterance (tests)
   int bneck_dbg = 0;           // VOXEMB_BNECK_DBG: timing experiments (skips work; wrong results)
   int chain_r = 0, chain_wpx = 0, chain_nw = 0;  // VOXEMB_CHAIN_R / VOXEMB_CHAIN_WPX (tuning)
@@ -809,7 +810,41 @@ static int build_res2net(Builder& B, const float* x, int n, int t, float* out) {
         emit_conv(B, c1a, cur, nullptr, 0, 1, 1, 1, 1, 0, 0, H, W, A, sw, EPI_AFFINE | EPI_RELU);
       }
       bool chained = false;
-      if (stride == 1 && m->dt == BF16 && !m->no_chain && w % 8 == 0) {
+      if (stride == 1 && m->dt == BF16 && !m->no_chain && !m->no_chain_rows &&
+          chain_rows_lds(w, s, W) > 0) {
+        // row-streamed chain (bneck.hip): no halo recompute
+        bool ok = s - 1 <= 8;
+        for (int j = 0; ok && j < s - 1; ++j)
+          ok = m->convs[ci + j].wtc && m->convs[ci + j].coutp >= 16 * ((w + 15) / 16);
+        if (ok) {
+          ChainParams q{};
+          q.a = A; q.lda = sw; q.b = Bc; q.ldb = sw;
+          q.N = n; q.H = H; q.W = W; q.w = w; q.nst = s - 1;
+          int nseg = 1;
+          while (n * nseg < 256 && H / (2 * nseg) >= 16) nseg *= 2;
+          q.R = (H + nseg - 1) / nseg;           // rows per segment
+          q.nwaves = (H + q.R - 1) / q.R;        // segments per utterance
+          double fl = 0;
+          for (int j = 0; j < s - 1; ++j) {
+            const ConvW& br = m->convs[ci + j];
+            q.wt[j] = br.wtc->p;
+            q.mean[j] = (const float*)br.mean->p;
+            q.inv[j] = (const float*)br.inv->p;
+            fl += 2.0 * n * H * W * 9.0 * w * w;
+          }
+          q.lds = chain_rows_lds(w, s, W);
+          Op op;
+          op.kind = OP_CONV;
+          op.type = 13;
+          op.ch = q;
+          op.flops = fl;
+          op.bytes = (double)es * n * H * W * w * (2.0 * (s - 1));
+          B.ops->push_back(op);
+          ci += s - 1;
+          chained = true;
+        }
+      }
+      if (!chained && stride == 1 && m->dt == BF16 && !m->no_chain && w % 8 == 0) {
         // fused split chain: all s-1 branches in one launch (kernels.hip split_chain)
         const ConvW& b0 = m->convs[ci];
         ChainParams q{};
@@ -1014,6 +1049,7 @@ static hipError_t run_op(vox_model* m, const Op& op, hipStream_t s) {
     case 9: return launch_gemm1x1(op.cp, s);
     case 10: return launch_split_chain(op.ch, op.cl.wco, op.cl.wpx, s);
     case 12: return launch_bneck(op.bq, op.cin, op.C, op.cl.wco, op.S, s);
+    case 13: return launch_chain_rows(op.ch, s);
     case 11:
       return launch_stem(m->dt, (const float*)op.src, op.N, op.H, op.W, op.part, op.C, op.mean,
                          op.inv, op.dst, s);
@@ -1077,6 +1113,7 @@ extern "C" int vox_load_blob(const void* blob, size_t nbytes, int device, int pr
   if (const char* e = std::getenv("VOXEMB_NO_CHAIN")) m->no_chain = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_NO_STEM")) m->no_stem = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_NO_BNECK")) m->no_bneck = std::atoi(e) != 0;
+  if (const char* e = std::getenv("VOXEMB_NO_CHAIN_ROWS")) m->no_chain_rows = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_BNECK_NSEG")) m->bneck_nseg = std::atoi(e);
   if (const char* e = std::getenv("VOXEMB_BNECK_DBG")) m->bneck_dbg = std::atoi(e);
   if (const char* e = std::getenv("VOXEMB_CHAIN_R")) m->chain_r = std::atoi(e);
@@ -1210,6 +1247,8 @@ extern "C" int vox_profile(vox_model* m, const float* d_x, int n, int t, int f, 
         tag |= (1 << 23);
       else if (o.type == 12)
         tag |= (1 << 24);
+      else if (o.type == 13)
+        tag |= (1 << 25);
       else if (o.type == 8)
         tag |= (o.cl.wco << 4) | (o.cl.wpx << 8) | (((o.cp.cinp + 31) / 32) << 16) | (1 << 20);
       else if (o.type == 0 || o.type == 5)
@@ -1231,7 +1270,7 @@ extern "C" int vox_plan_describe(vox_model* m, const float* d_x, int n, int t, i
   if ((rc = ensure_plan(m, d_x, n, t, (float*)m->stage_out.p))) return rc;
   std::string out;
   static const char* tn[] = {"igemm", "reduce", "pool", "avgpool", "convert", "igemm32", "bnrelu",
-                             "win", "rr", "gemm", "chain", "stem", "bneck"};
+                             "win", "rr", "gemm", "chain", "stem", "bneck", "chainrows"};
   for (const Op& o : m->plan) {
     char line[256];
     const ConvParams& p = o.cp;
@@ -1246,6 +1285,10 @@ extern "C" int vox_plan_describe(vox_model* m, const float* d_x, int n, int t, i
       std::snprintf(line, sizeof(line), "bneck N=%d H=%d W=%d Cin=%d C=%d w=%d split=%d seg=%d nseg=%d flops=%.4g bytes=%.4g\n",
                     o.bq.N, o.bq.H, o.bq.W, o.cin, o.C, o.cl.wco, o.S, o.bq.seg, o.bq.nseg, o.flops,
                     o.bytes);
+    else if (o.type == 13)
+      std::snprintf(line, sizeof(line), "chainrows N=%d H=%d W=%d w=%d nst=%d seg=%d nseg=%d lds=%d flops=%.4g bytes=%.4g\n",
+                    o.ch.N, o.ch.H, o.ch.W, o.ch.w, o.ch.nst, o.ch.R, o.ch.nwaves, o.ch.lds,
+                    o.flops, o.bytes);
     else if (o.type == 10)
       std::snprintf(line, sizeof(line), "chain wco=%d wpx=%d N=%d H=%d W=%d w=%d nst=%d R=%d lds=%d flops=%.4g bytes=%.4g\n",
                     o.cl.wco, o.cl.wpx, o.ch.N, o.ch.H, o.ch.W, o.ch.w, o.ch.nst, o.ch.R, o.ch.lds,

@@ -449,3 +449,219 @@ hipError_t launch_bneck(const BneckParams& q, int CI, int C, int wid, int s, hip
 }
 
 }  // namespace vox
+
+namespace vox {
+
+// ----------------------------------------------------------------------------
+// Row-streamed Res2Net split chain (stride 1) for blocks the whole-bottleneck
+// kernel cannot hold (wider branches): the 1x1a output planes x_1..x_{S-1}
+// stream in row by row, every 3x3 stage runs in one phase on its own lagged
+// row (stage k on row a-2k+1, as in bneck_fused), z_{k+1} = x_{k+1} + y_k
+// stays in LDS rings and y_k goes to HBM.  No halo rows are recomputed
+// (split_chain's row tiles recompute 2(S-2) of every R+... rows).
+// Waves: one per (stage, cout tile) with its weights in registers; NW is the
+// role count rounded up to whole SIMDs (spare waves only move data).
+template <int WID, int S, int PT>
+struct ChainRowsCfg {
+  static constexpr int WCO = (WID + 15) / 16;
+  static constexpr int ROLES = (S - 1) * WCO;
+  static constexpr int NW = (ROLES + 3) / 4 * 4;
+  static constexpr int NT = 64 * NW;
+  static constexpr int KFLAT = 9 * WID;
+  static constexpr int KST = (KFLAT + 31) / 32;
+  static constexpr int AU = ((WID / 8) & 1) ? WID / 8 : WID / 8 + 1;
+  static constexpr int ASTR = AU * 16;
+  static constexpr int WR = 16 * PT + 2;
+  static constexpr int ROWB = WR * ASTR;
+  // z_1: 3 rows, z_k: 4 rows (k = 2..S-1); x_k: 2k-2 rows (k = 2..S-1)
+  static constexpr int ZEND = 3 + 4 * (S - 2);
+  static constexpr int NPLANES = ZEND + (S - 2) * (S - 1);
+  static constexpr int RING_BYTES = NPLANES * ROWB;
+  static constexpr int LDS = RING_BYTES + 4 * 2 * (S - 1) * 16 * WCO;
+  static constexpr int CU = (S - 1) * WID / 8;               // 16-B chunks of x_1..x_{S-1}
+  static constexpr int XREG = (16 * PT * CU + NT - 1) / NT;  // per thread
+};
+
+template <int WID, int S, int PT>
+__global__ __launch_bounds__((ChainRowsCfg<WID, S, PT>::NT)) void chain_rows(ChainParams q) {
+  using K = ChainRowsCfg<WID, S, PT>;
+  constexpr int NT = K::NT, WCO = K::WCO, KST = K::KST, ASTR = K::ASTR, ROWB = K::ROWB;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int col = lane & 15, g = lane >> 4;
+  const int H = q.H, W = q.W;
+  const int nseg = q.nwaves;                 // segments per utterance (reused field)
+  const int n = blockIdx.x / nseg;
+  const int h0 = (blockIdx.x - n * nseg) * q.R;
+  const int h1 = min(H, h0 + q.R);
+  char* rings = smem;
+  float* bmb = reinterpret_cast<float*>(smem + K::RING_BYTES);
+  float* bib = bmb + (S - 1) * 16 * WCO;
+  const bf16_t* __restrict__ A = reinterpret_cast<const bf16_t*>(q.a);
+  bf16_t* __restrict__ Bo = reinterpret_cast<bf16_t*>(q.b);
+  const size_t img = (size_t)n * H * W;
+
+  for (int i = tid; i < K::RING_BYTES / 16; i += NT)
+    reinterpret_cast<uint4*>(rings)[i] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+  for (int k = 0; k < S - 1; ++k)
+    for (int c = tid; c < 16 * WCO; c += NT) {
+      bmb[k * 16 * WCO + c] = c < WID ? q.mean[k][c] : 0.f;
+      bib[k * 16 * WCO + c] = c < WID ? q.inv[k][c] : 0.f;
+    }
+
+  const bool role = wave < K::ROLES;
+  const int ck = role ? wave / WCO + 1 : 1;
+  const int ci = wave % WCO;
+  bf16x8 wb[KST];
+  {
+    const void* wk = q.wt[0];
+#pragma unroll
+    for (int k = 1; k < S - 1; ++k)
+      if (ck == k + 1) wk = q.wt[k];
+    const bf16_t* __restrict__ Wk = reinterpret_cast<const bf16_t*>(wk);
+#pragma unroll
+    for (int s = 0; s < KST; ++s) {
+      const int kk = 32 * s + 8 * g;
+      wb[s] = (role && kk < K::KFLAT) ? ld16(Wk + (size_t)(ci * 16 + col) * K::KFLAT + kk)
+                                      : bf16x8{};
+    }
+  }
+  int ktab[KST];
+#pragma unroll
+  for (int s = 0; s < KST; ++s) {
+    const int kk = 32 * s + 8 * g;
+    int dyi = 1, off = 0;
+    if (kk < K::KFLAT) {
+      const int tap = kk / WID, ch = kk - tap * WID;
+      dyi = tap / 3;
+      off = (tap % 3 - 1) * ASTR + ch * 2;
+    }
+    ktab[s] = (dyi << 24) | (off + 32768);
+  }
+
+  // x rows: global -> registers one step ahead -> LDS rings
+  uint4 xr[K::XREG];
+  auto load_x = [&](int r) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < K::XREG; ++i) {
+      const int c = tid + i * NT;
+      const int px = c / K::CU, u = c - px * K::CU;
+      xr[i] = make_uint4(0, 0, 0, 0);
+      if (c < 16 * PT * K::CU && px < W && r >= 0 && r < H)
+        xr[i] = *reinterpret_cast<const uint4*>(A + (img + (size_t)r * W + px) * q.lda + u * 8);
+    }
+  };
+  auto store_x = [&](int r) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < K::XREG; ++i) {
+      const int c = tid + i * NT;
+      const int px = c / K::CU, u = c - px * K::CU;
+      if (c < 16 * PT * K::CU && px < W) {
+        const int ch = u * 8, p = ch / WID, off = ch - p * WID;
+        int sl = (r + 840) % 3;                         // plane 0 -> z_1
+#pragma unroll
+        for (int d = 2; d < S; ++d)
+          if (p + 1 == d) sl = K::ZEND + (d - 2) * (d - 1) + (r + 840) % (2 * d - 2);
+        *reinterpret_cast<uint4*>(rings + sl * ROWB + (px + 1) * ASTR + off * 2) = xr[i];
+      }
+    }
+  };
+
+  const int a0 = h0 - (S - 1);
+  const int steps = (h1 - h0) + 3 * (S - 1) - 1;  // stage S-1 reaches row h1-1 at a = h1+2S-4
+  load_x(a0);
+  for (int t = 0; t < steps; ++t) {
+    const int a = a0 + t;
+    store_x(a);
+    __syncthreads();
+    load_x(a + 1);
+    if (role) {
+      const int k = ck;
+      const int co = 16 * ci + 4 * g;
+      const int r = a - 2 * k + 1;
+      const bool inimg = r >= 0 && r < H;
+      const int zd = k == 1 ? 3 : 4;
+      const int zbase = k == 1 ? 0 : 3 + 4 * (k - 2);
+      const int rb0 = __builtin_amdgcn_readfirstlane((zbase + (r - 1 + 840) % zd) * ROWB);
+      const int rb1 = __builtin_amdgcn_readfirstlane((zbase + (r + 840) % zd) * ROWB);
+      const int rb2 = __builtin_amdgcn_readfirstlane((zbase + (r + 1 + 840) % zd) * ROWB);
+      const bool chain_next = k < S - 1;
+      const int zsl = __builtin_amdgcn_readfirstlane((3 + 4 * (k - 1) + (r + 840) % 4) * ROWB);
+      const int xsl = __builtin_amdgcn_readfirstlane(
+          (K::ZEND + (k - 1) * k + (r + 840) % (2 * k)) * ROWB);
+      const f32x4 m = *reinterpret_cast<const f32x4*>(bmb + (k - 1) * 16 * WCO + co);
+      const f32x4 sc = *reinterpret_cast<const f32x4*>(bib + (k - 1) * 16 * WCO + co);
+      const bool emit = r >= h0 && r < h1;               // rows this segment owns
+      int boff[KST];
+#pragma unroll
+      for (int s = 0; s < KST; ++s) {
+        int e = ktab[s];
+        asm volatile("" : "+v"(e));
+        const int dyi = e >> 24;
+        boff[s] = (dyi == 0 ? rb0 : (dyi == 1 ? rb1 : rb2)) + (e & 0xFFFFFF) - 32768 + ASTR;
+      }
+      auto epilogue = [&](const f32x4& acc, int px) __attribute__((always_inline)) {
+        if (!(co < WID && px < W)) return;
+        const int pxo = px * ASTR + co * 2 + ASTR;
+        bf16x4 y;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) y[e] = (bf16_t)fmaxf((acc[e] - m[e]) * sc[e], 0.f);
+        if (emit)
+          *reinterpret_cast<bf16x4*>(Bo + (img + (size_t)r * W + px) * q.ldb + (k - 1) * WID + co) = y;
+        if (chain_next) {
+          const bf16x4 x = *reinterpret_cast<const bf16x4*>(rings + xsl + pxo);
+          *reinterpret_cast<bf16x4*>(rings + zsl + pxo) = inimg ? add4(x, y) : bf16x4{};
+        }
+      };
+      for (int j = 0; j < PT; j += 2) {
+        const bool two = j + 1 < PT;
+        const int px0 = 16 * j + col, px1 = px0 + 16;
+        bf16x8 b0[KST], b1[KST];
+#pragma unroll
+        for (int s = 0; s < KST; ++s) {
+          b0[s] = *reinterpret_cast<const bf16x8*>(rings + boff[s] + px0 * ASTR);
+          b1[s] = two ? *reinterpret_cast<const bf16x8*>(rings + boff[s] + px1 * ASTR) : bf16x8{};
+        }
+        f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < KST; ++s) {
+          acc0 = mfma_step(wb[s], b0[s], acc0);
+          acc1 = mfma_step(wb[s], b1[s], acc1);
+        }
+        epilogue(acc0, px0);
+        if (two) epilogue(acc1, px1);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+#define CHAIN_ROWS_SHAPES(X) \
+  X(48, 4, 3)  /* res2net50_w24_s4_c32 layer 2, 80-d features (W = 40) */ \
+  X(48, 4, 2)  /* ... 40-d features (W = 20) */
+
+int chain_rows_lds(int wid, int s, int W) {
+  const int pt = (W + 15) / 16;
+#define X_LDS(w_, s_, p_) \
+  if (wid == w_ && s == s_ && pt == p_) return ChainRowsCfg<w_, s_, p_>::LDS;
+  CHAIN_ROWS_SHAPES(X_LDS)
+#undef X_LDS
+  return -1;
+}
+
+hipError_t launch_chain_rows(const ChainParams& q, hipStream_t st) {
+  const int pt = (q.W + 15) / 16;
+#define X_LAUNCH(w_, s_, p_)                                                             \
+  if (q.w == w_ && q.nst + 1 == s_ && pt == p_) {                                      \
+    using K = ChainRowsCfg<w_, s_, p_>;                                                \
+    hipLaunchKernelGGL((chain_rows<w_, s_, p_>), dim3(q.N * q.nwaves), dim3(K::NT), K::LDS, \
+                       st, q);                                                         \
+    return hipGetLastError();                                                          \
+  }
+  CHAIN_ROWS_SHAPES(X_LAUNCH)
+#undef X_LAUNCH
+  return hipErrorInvalidValue;
+}
+
+}  // namespace vox

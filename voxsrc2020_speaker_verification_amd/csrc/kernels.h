@@ -60,6 +60,10 @@ struct ChainParams {
   int nwaves;                       // 4 or 8 waves per block
 };
 hipError_t launch_split_chain(const ChainParams& q, int wco, int wpx, hipStream_t s);
+// Row-streamed split chain (bneck.hip): utterance segments of q.R rows, q.nwaves
+// segments per utterance (grid N * q.nwaves); LDS bytes or -1 if no instance.
+int chain_rows_lds(int w, int split, int W);
+hipError_t launch_chain_rows(const ChainParams& q, hipStream_t s);
 
 // Fused Res2Net bottleneck (stride 1): 1x1a + split chain + 1x1c + identity
 // or 1x1-projection shortcut in one launch, intermediates in LDS ring
