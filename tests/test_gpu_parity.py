@@ -178,8 +178,9 @@ def test_extract_cli_end_to_end(weights, tmp_path):
 
 
 @pytest.mark.parametrize("unfused_env", [("VOXEMB_NO_BNECK",), ("VOXEMB_NO_CHAIN_ROWS",),
-                                         ("VOXEMB_NO_BNECK", "VOXEMB_NO_CHAIN")],
-                         ids=["chain", "tiled_chain", "unfused"])
+                                         ("VOXEMB_NO_SPLIT_S2",),
+                                         ("VOXEMB_NO_BNECK", "VOXEMB_NO_CHAIN", "VOXEMB_NO_SPLIT_S2")],
+                         ids=["chain", "tiled_chain", "split_s2", "unfused"])
 @pytest.mark.parametrize("name,F,T,N", [("res2net50_w24_s4_c32", 80, 200, 3),
                                         ("res2net50_w24_s4_c32", 80, 37, 3),
                                         ("res2net50_w24_s4_c32", 40, 75, 2),

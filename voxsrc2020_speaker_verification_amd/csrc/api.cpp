@@ -224,6 +224,7 @@ struct vox_model {
   bool no_stem = false;        // VOXEMB_NO_STEM=1: stem through the generic conv
   bool no_bneck = false;       // VOXEMB_NO_BNECK=1: unfused identity bottlenecks
   bool no_chain_rows = false;  // VOXEMB_NO_CHAIN_ROWS=1: row-tiled split_chain instead
+  bool no_split_s2 = false;    // VOXEMB_NO_SPLIT_S2=1: stride-2 branches as separate convs
   int bneck_nseg = 0;          // VOXEMB_BNECK_NSEG: force row segments per utterance (tests)
   int bneck_dbg = 0;           // VOXEMB_BNECK_DBG: timing experiments (skips work; wrong results)
   int chain_r = 0, chain_wpx = 0, chain_nw = 0;  // VOXEMB_CHAIN_R / VOXEMB_CHAIN_WPX (tuning)
@@ -897,6 +898,38 @@ static int build_res2net(Builder& B, const float* x, int n, int t, float* out) {
           chained = true;
         }
       }
+      bool pooled = false;
+      if (stride == 2 && m->dt == BF16 && !m->no_split_s2 && split_s2_lds(w, s, W) > 0) {
+        // all stride-2 branches + the last split's avg pool in one launch (bneck.hip)
+        bool ok = s - 1 <= 8;
+        for (int j = 0; ok && j < s - 1; ++j)
+          ok = m->convs[ci + j].wtc && m->convs[ci + j].coutp >= 16 * ((w + 15) / 16);
+        if (ok) {
+          ChainParams q{};
+          q.a = A; q.lda = sw; q.b = Bc; q.ldb = sw;
+          q.N = n; q.H = H; q.W = W; q.w = w; q.nst = s - 1;
+          int nseg = 1;
+          while (n * nseg < 256 && Ho / (2 * nseg) >= 8) nseg *= 2;
+          q.R = (Ho + nseg - 1) / nseg;
+          q.nwaves = (Ho + q.R - 1) / q.R;
+          for (int j = 0; j < s - 1; ++j) {
+            const ConvW& br = m->convs[ci + j];
+            q.wt[j] = br.wtc->p;
+            q.mean[j] = (const float*)br.mean->p;
+            q.inv[j] = (const float*)br.inv->p;
+          }
+          q.lds = split_s2_lds(w, s, W);
+          Op op;
+          op.kind = OP_CONV;
+          op.type = 14;
+          op.ch = q;
+          op.flops = 2.0 * n * Ho * Wo * 9.0 * w * w * (s - 1);
+          op.bytes = (double)es * ((double)n * H * W * sw + (double)n * Ho * Wo * sw);
+          B.ops->push_back(op);
+          ci += s - 1;
+          chained = pooled = true;
+        }
+      }
       for (int j = 0; !chained && j < s - 1; ++j) {  // res2net_pad_conv_bn_relu :53-75
         const ConvW& br = m->convs[ci++];
         Act xin{A ? A + (size_t)j * w * es : nullptr, sw, n, H, W, w};
@@ -906,7 +939,7 @@ static int build_res2net(Builder& B, const float* x, int n, int t, float* out) {
         emit_conv(B, br, xin, add, sw, stride, stride, 1, 1, 1, 1, Ho, Wo, yb, sw,
                   EPI_AFFINE | EPI_RELU);
       }
-      if (stride != 1) {  // last split: AvgPool 3x3/2 VALID on the padded tensor (:77)
+      if (stride != 1 && !pooled) {  // last split: AvgPool 3x3/2 VALID on the padded tensor (:77)
         Op op;
         op.kind = OP_OTHER;
         op.type = 3;
@@ -1050,6 +1083,7 @@ static hipError_t run_op(vox_model* m, const Op& op, hipStream_t s) {
     case 10: return launch_split_chain(op.ch, op.cl.wco, op.cl.wpx, s);
     case 12: return launch_bneck(op.bq, op.cin, op.C, op.cl.wco, op.S, s);
     case 13: return launch_chain_rows(op.ch, s);
+    case 14: return launch_split_s2(op.ch, s);
     case 11:
       return launch_stem(m->dt, (const float*)op.src, op.N, op.H, op.W, op.part, op.C, op.mean,
                          op.inv, op.dst, s);
@@ -1114,6 +1148,7 @@ extern "C" int vox_load_blob(const void* blob, size_t nbytes, int device, int pr
   if (const char* e = std::getenv("VOXEMB_NO_STEM")) m->no_stem = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_NO_BNECK")) m->no_bneck = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_NO_CHAIN_ROWS")) m->no_chain_rows = std::atoi(e) != 0;
+  if (const char* e = std::getenv("VOXEMB_NO_SPLIT_S2")) m->no_split_s2 = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_BNECK_NSEG")) m->bneck_nseg = std::atoi(e);
   if (const char* e = std::getenv("VOXEMB_BNECK_DBG")) m->bneck_dbg = std::atoi(e);
   if (const char* e = std::getenv("VOXEMB_CHAIN_R")) m->chain_r = std::atoi(e);
@@ -1249,6 +1284,8 @@ extern "C" int vox_profile(vox_model* m, const float* d_x, int n, int t, int f, 
         tag |= (1 << 24);
       else if (o.type == 13)
         tag |= (1 << 25);
+      else if (o.type == 14)
+        tag |= (1 << 26);
       else if (o.type == 8)
         tag |= (o.cl.wco << 4) | (o.cl.wpx << 8) | (((o.cp.cinp + 31) / 32) << 16) | (1 << 20);
       else if (o.type == 0 || o.type == 5)
@@ -1270,7 +1307,7 @@ extern "C" int vox_plan_describe(vox_model* m, const float* d_x, int n, int t, i
   if ((rc = ensure_plan(m, d_x, n, t, (float*)m->stage_out.p))) return rc;
   std::string out;
   static const char* tn[] = {"igemm", "reduce", "pool", "avgpool", "convert", "igemm32", "bnrelu",
-                             "win", "rr", "gemm", "chain", "stem", "bneck", "chainrows"};
+                             "win", "rr", "gemm", "chain", "stem", "bneck", "chainrows", "splits2"};
   for (const Op& o : m->plan) {
     char line[256];
     const ConvParams& p = o.cp;
@@ -1285,6 +1322,10 @@ extern "C" int vox_plan_describe(vox_model* m, const float* d_x, int n, int t, i
       std::snprintf(line, sizeof(line), "bneck N=%d H=%d W=%d Cin=%d C=%d w=%d split=%d seg=%d nseg=%d flops=%.4g bytes=%.4g\n",
                     o.bq.N, o.bq.H, o.bq.W, o.cin, o.C, o.cl.wco, o.S, o.bq.seg, o.bq.nseg, o.flops,
                     o.bytes);
+    else if (o.type == 14)
+      std::snprintf(line, sizeof(line), "splits2 N=%d H=%d W=%d w=%d nst=%d seg=%d nseg=%d lds=%d flops=%.4g bytes=%.4g\n",
+                    o.ch.N, o.ch.H, o.ch.W, o.ch.w, o.ch.nst, o.ch.R, o.ch.nwaves, o.ch.lds,
+                    o.flops, o.bytes);
     else if (o.type == 13)
       std::snprintf(line, sizeof(line), "chainrows N=%d H=%d W=%d w=%d nst=%d seg=%d nseg=%d lds=%d flops=%.4g bytes=%.4g\n",
                     o.ch.N, o.ch.H, o.ch.W, o.ch.w, o.ch.nst, o.ch.R, o.ch.nwaves, o.ch.lds,

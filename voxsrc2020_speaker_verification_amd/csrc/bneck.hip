@@ -665,3 +665,247 @@ hipError_t launch_chain_rows(const ChainParams& q, hipStream_t st) {
 }
 
 }  // namespace vox
+
+namespace vox {
+
+// ----------------------------------------------------------------------------
+// Stride-2 Res2Net split ('stage' blocks, res2net_model.py:53-77): branch k
+// (k < S) = relu(bn(conv3x3 stride 2, fixed pad 1)(x_k)), the last split
+// avg-pooled 3x3/2 (divisor 9), all from one row-streamed launch.  Output row
+// ho reads input rows 2ho-1..2ho+1 of every plane from a 3-row LDS ring; the
+// next two input rows stream in (global -> registers -> LDS) while the row is
+// computed.  Waves: one per (branch, cout tile) with weights in registers;
+// the spare waves average-pool the last plane.
+template <int WID, int S, int WIN>
+struct SplitS2Cfg {
+  static constexpr int WOUT = (WIN + 1) / 2;
+  static constexpr int PT = (WOUT + 15) / 16;
+  static constexpr int WR = WIN + 2;            // ring row: pad | WIN | pad
+  static constexpr int WCO = (WID + 15) / 16;
+  static constexpr int ROLES = (S - 1) * WCO;
+  static constexpr int NW = (ROLES + 3) / 4 * 4 + ((ROLES % 4) == 0 ? 4 : 0);  // >= 1 spare wave
+  static constexpr int NT = 64 * NW;
+  static constexpr int KFLAT = 9 * WID;
+  static constexpr int KST = (KFLAT + 31) / 32;
+  static constexpr int AU = ((WID / 8) & 1) ? WID / 8 : WID / 8 + 1;
+  static constexpr int ASTR = AU * 16;
+  static constexpr int CU = S * WID / 8;        // 16-B chunks per input pixel (all planes)
+  static constexpr int WC8 = WID / 8;           // chunks of one plane
+  static constexpr int XREG = (2 * WIN * CU + NT - 1) / NT;   // two rows per step
+  static constexpr int LDS = S * 3 * WR * ASTR + 4 * 2 * (S - 1) * 16 * WCO + 4 * 4 * KST;
+};
+
+template <int WID, int S, int WIN>
+__global__ __launch_bounds__((SplitS2Cfg<WID, S, WIN>::NT)) void split_s2_rows(ChainParams q) {
+  using K = SplitS2Cfg<WID, S, WIN>;
+  constexpr int NT = K::NT, WCO = K::WCO, KST = K::KST, ASTR = K::ASTR, CU = K::CU;
+  constexpr int PT = K::PT, W = WIN, Wo = K::WOUT, ROWB = K::WR * ASTR, PLANEB = 3 * ROWB;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int col = lane & 15, g = lane >> 4;
+  const int H = q.H;
+  const int Ho = (H + 1) / 2;
+  const int nseg = q.nwaves;
+  const int n = blockIdx.x / nseg;
+  const int g0 = (blockIdx.x - n * nseg) * q.R;
+  const int g1 = min(Ho, g0 + q.R);
+  char* rings = smem;
+  const int ring_bytes = S * PLANEB;
+  float* bmb = reinterpret_cast<float*>(smem + ring_bytes);
+  float* bib = bmb + (S - 1) * 16 * WCO;
+  int* ktab_l = reinterpret_cast<int*>(bib + (S - 1) * 16 * WCO);   // [4 lane groups][KST]
+  const bf16_t* __restrict__ A = reinterpret_cast<const bf16_t*>(q.a);
+  bf16_t* __restrict__ Bo = reinterpret_cast<bf16_t*>(q.b);
+  const size_t img = (size_t)n * H * W;
+  const size_t imgo = (size_t)n * Ho * Wo;
+
+  for (int i = tid; i < ring_bytes / 16; i += NT)
+    reinterpret_cast<uint4*>(rings)[i] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+  for (int k = 0; k < S - 1; ++k)
+    for (int c = tid; c < 16 * WCO; c += NT) {
+      bmb[k * 16 * WCO + c] = c < WID ? q.mean[k][c] : 0.f;
+      bib[k * 16 * WCO + c] = c < WID ? q.inv[k][c] : 0.f;
+    }
+
+  const bool role = wave < K::ROLES;
+  const int ck = role ? wave / WCO : 0;          // branch (0-based)
+  const int ci = wave % WCO;
+  bf16x8 wb[KST];
+  {
+    const void* wk = q.wt[0];
+#pragma unroll
+    for (int k = 1; k < S - 1; ++k)
+      if (ck == k) wk = q.wt[k];
+    const bf16_t* __restrict__ Wk = reinterpret_cast<const bf16_t*>(wk);
+#pragma unroll
+    for (int s = 0; s < KST; ++s) {
+      const int kk = 32 * s + 8 * g;
+      wb[s] = (role && kk < K::KFLAT) ? ld16(Wk + (size_t)(ci * 16 + col) * K::KFLAT + kk)
+                                      : bf16x8{};
+    }
+  }
+  // k-step table per lane group (LDS; read back every row): tap row << 24 |
+  // (byte offset + 2^15)
+  for (int i = tid; i < 4 * KST; i += NT) {
+    const int gg = i / KST, s = i - gg * KST;
+    const int kk = 32 * s + 8 * gg;
+    int dyi = 1, off = 0;
+    if (kk < K::KFLAT) {
+      const int tap = kk / WID, ch = kk - tap * WID;
+      dyi = tap / 3;
+      off = (tap % 3 - 1) * ASTR + ch * 2;
+    }
+    ktab_l[i] = (dyi << 24) | (off + 32768);
+  }
+
+  // two input rows per step: global -> registers -> ring.  Chunk c of the
+  // pair is (row rr, pixel px, 16-B unit u); all divisors are compile-time and
+  // addresses are a scalar row base + a 32-bit lane offset (nothing to hoist).
+  constexpr int XREG = K::XREG;
+  uint4 xr[XREG];
+  const int lda = q.lda;
+  auto load_rows = [&](int r0) __attribute__((always_inline)) {
+    const bf16_t* base = A + (img + (size_t)r0 * W) * lda;
+#pragma unroll
+    for (int i = 0; i < XREG; ++i) {
+      const int c = tid + i * NT;
+      const int rr = c / (W * CU), cc = c - rr * (W * CU);
+      const int px = cc / CU, u = cc - px * CU;
+      const int r = r0 + rr;
+      xr[i] = make_uint4(0, 0, 0, 0);
+      if (rr < 2 && r >= 0 && r < H)
+        xr[i] = *reinterpret_cast<const uint4*>(base + (rr * W + px) * lda + u * 8);
+    }
+  };
+  auto store_rows = [&](int r0, int nrows) __attribute__((always_inline)) {
+    const int s0 = ((r0 + 840) % 3) * ROWB, s1 = ((r0 + 841) % 3) * ROWB;
+#pragma unroll
+    for (int i = 0; i < XREG; ++i) {
+      const int c = tid + i * NT;
+      const int rr = c / (W * CU), cc = c - rr * (W * CU);
+      const int px = cc / CU, u = cc - px * CU;
+      if (rr < nrows) {
+        const int p = u / K::WC8, uo = u - p * K::WC8;
+        *reinterpret_cast<uint4*>(rings + p * PLANEB + (rr ? s1 : s0) + (px + 1) * ASTR + uo * 16) =
+            xr[i];
+      }
+    }
+  };
+
+  load_rows(2 * g0 - 1);       // row 2*g0-1 (first of the pair) seeds the ring
+  store_rows(2 * g0 - 1, 1);
+  load_rows(2 * g0);
+  for (int ho = g0; ho < g1; ++ho) {
+    store_rows(2 * ho, 2);
+    __syncthreads();
+    load_rows(2 * ho + 2);
+    const int rb0 = __builtin_amdgcn_readfirstlane(((2 * ho - 1 + 840) % 3) * ROWB);
+    const int rb1 = __builtin_amdgcn_readfirstlane(((2 * ho + 840) % 3) * ROWB);
+    const int rb2 = __builtin_amdgcn_readfirstlane(((2 * ho + 1 + 840) % 3) * ROWB);
+    if (role) {
+      const int co = 16 * ci + 4 * g;
+      const char* zb = rings + ck * PLANEB;
+      const f32x4 m = *reinterpret_cast<const f32x4*>(bmb + ck * 16 * WCO + co);
+      const f32x4 sc = *reinterpret_cast<const f32x4*>(bib + ck * 16 * WCO + co);
+      int boff[KST];
+#pragma unroll
+      for (int s = 0; s < KST; ++s) {
+        const int e = ktab_l[g * KST + s];
+        const int dyi = e >> 24;
+        boff[s] = (dyi == 0 ? rb0 : (dyi == 1 ? rb1 : rb2)) + (e & 0xFFFFFF) - 32768 + ASTR;
+      }
+      auto epilogue = [&](const f32x4& acc, int wo) __attribute__((always_inline)) {
+        if (!(co < WID && wo < Wo)) return;
+        bf16x4 y;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) y[e] = (bf16_t)fmaxf((acc[e] - m[e]) * sc[e], 0.f);
+        *reinterpret_cast<bf16x4*>(Bo + (imgo + (size_t)ho * Wo + wo) * q.ldb + ck * WID + co) = y;
+      };
+      for (int j = 0; j < PT; j += 2) {
+        const bool two = j + 1 < PT;
+        const int wo0 = 16 * j + col, wo1 = wo0 + 16;
+        f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+        constexpr int KH = (KST + 1) / 2;   // B fragments in two halves (register budget)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          bf16x8 b0[KH], b1[KH];
+#pragma unroll
+          for (int i = 0; i < KH; ++i) {
+            const int s = h * KH + i;
+            if (s < KST) {
+              b0[i] = *reinterpret_cast<const bf16x8*>(zb + boff[s] + 2 * min(wo0, Wo - 1) * ASTR);
+              b1[i] = two ? *reinterpret_cast<const bf16x8*>(zb + boff[s] + 2 * min(wo1, Wo - 1) * ASTR)
+                          : bf16x8{};
+            }
+          }
+#pragma unroll
+          for (int i = 0; i < KH; ++i) {
+            const int s = h * KH + i;
+            if (s < KST) {
+              acc0 = mfma_step(wb[s], b0[i], acc0);
+              acc1 = mfma_step(wb[s], b1[i], acc1);
+            }
+          }
+        }
+        epilogue(acc0, wo0);
+        if (two) epilogue(acc1, wo1);
+      }
+    } else {
+      // last split: AvgPool 3x3/2 VALID over the fixed-padded plane, divisor 9
+      // (taps outside the image skipped, in the order of avgpool3s2_v8)
+      const char* pl = rings + (S - 1) * PLANEB;
+      const int st = tid - 64 * K::ROLES, nst = NT - 64 * K::ROLES;
+      for (int it = st; it < Wo * K::WC8; it += nst) {
+        const int wo = it / K::WC8, u = it - wo * K::WC8;
+        float sum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) {
+          const int hi = 2 * ho - 1 + ky;
+          if (hi < 0 || hi >= H) continue;
+          const int rb = ky == 0 ? rb0 : (ky == 1 ? rb1 : rb2);
+#pragma unroll
+          for (int kx = 0; kx < 3; ++kx) {
+            const int wi = 2 * wo - 1 + kx;
+            if (wi < 0 || wi >= W) continue;
+            const bf16x8 v = *reinterpret_cast<const bf16x8*>(pl + rb + (wi + 1) * ASTR + u * 16);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) sum[e] += (float)v[e];
+          }
+        }
+        bf16x8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = (bf16_t)(sum[e] / 9.0f);
+        *reinterpret_cast<bf16x8*>(Bo + (imgo + (size_t)ho * Wo + wo) * q.ldb + (S - 1) * WID + u * 8) = o;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+#define SPLIT_S2_SHAPES(X) \
+  X(48, 4, 80)  /* res2net50_w24_s4_c32 layer-2 block 0, 80-d features */ \
+  X(48, 4, 40)  /* ... 40-d features */
+
+int split_s2_lds(int wid, int s, int W) {
+#define X_LDS(w_, s_, win_) \
+  if (wid == w_ && s == s_ && W == win_) return SplitS2Cfg<w_, s_, win_>::LDS;
+  SPLIT_S2_SHAPES(X_LDS)
+#undef X_LDS
+  return -1;
+}
+
+hipError_t launch_split_s2(const ChainParams& q, hipStream_t st) {
+#define X_LAUNCH(w_, s_, win_)                                                             \
+  if (q.w == w_ && q.nst + 1 == s_ && q.W == win_) {                                     \
+    using K = SplitS2Cfg<w_, s_, win_>;                                                  \
+    hipLaunchKernelGGL((split_s2_rows<w_, s_, win_>), dim3(q.N * q.nwaves), dim3(K::NT), \
+                       K::LDS, st, q);                                                   \
+    return hipGetLastError();                                                            \
+  }
+  SPLIT_S2_SHAPES(X_LAUNCH)
+#undef X_LAUNCH
+  return hipErrorInvalidValue;
+}
+
+}  // namespace vox

@@ -64,6 +64,11 @@ hipError_t launch_split_chain(const ChainParams& q, int wco, int wpx, hipStream_
 // segments per utterance (grid N * q.nwaves); LDS bytes or -1 if no instance.
 int chain_rows_lds(int w, int split, int W);
 hipError_t launch_chain_rows(const ChainParams& q, hipStream_t s);
+// Stride-2 split (bneck.hip): branches k < split-1 (3x3 s2 + BN + ReLU) and the
+// last split's 3x3/2 average pool, q.R output rows per segment, q.nwaves
+// segments per utterance; q.H/q.W are the INPUT dims.  LDS bytes or -1.
+int split_s2_lds(int w, int split, int W);
+hipError_t launch_split_s2(const ChainParams& q, hipStream_t s);
 
 // Fused Res2Net bottleneck (stride 1): 1x1a + split chain + 1x1c + identity
 // or 1x1-projection shortcut in one launch, intermediates in LDS ring
