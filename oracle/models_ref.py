@@ -118,6 +118,25 @@ def stats_pool(x, eps=STATS_EPS):
     return np.concatenate([mean, std], axis=3).astype(np.float32)
 
 
+def att_stats_pool(x, k1, k2, eps=STATS_EPS):
+    """models.py:273-303 (att_with_mean_std=True): moments over H, att input =
+    concat[x, tile(mean), tile(std)] on C, logits = conv1x1(tanh(conv1x1(.)))
+    (no bias), softmax over H, weighted mean and sqrt(E_w[x^2] - mean^2 + eps).
+    x: [N,H,W,C] -> [N,1,W,2C]."""
+    m = stats_pool(x, eps)                                   # [N,1,W,2C]
+    tiled = np.broadcast_to(m, x.shape[:3] + (m.shape[3],))
+    a = np.concatenate([x, tiled], axis=3).astype(np.float32)
+    h = np.tanh(a @ k1[0, 0]).astype(np.float32)
+    logits = (h @ k2[0, 0]).astype(np.float32)
+    z = logits - logits.max(axis=1, keepdims=True)
+    e = np.exp(z).astype(np.float32)
+    w = (e / e.sum(axis=1, keepdims=True)).astype(np.float32)
+    wm = (x * w).sum(axis=1, keepdims=True, dtype=np.float32)
+    wss = (x * x * w).sum(axis=1, keepdims=True, dtype=np.float32)
+    ws = np.sqrt(wss - wm * wm + np.float32(eps)).astype(np.float32)
+    return np.concatenate([wm, ws], axis=3).astype(np.float32)
+
+
 def flatten_nhwc(x):
     """tf.compat.v1.layers.flatten on NHWC: feature index = (h*W + w)*C + c."""
     return x.reshape(x.shape[0], -1)
@@ -227,7 +246,10 @@ def res2net_forward(spec, tensors, x):
             h = res2net_split_conv(h, kern, bns, stride, s, w)
             h = batch_norm(conv2d_fixed_padding(h, p.conv(), 1), *p.bn())
             x = relu(h + sc)
-    x = flatten_nhwc(stats_pool(x))
+    if spec.get("pool") == "att":                            # res2net_model.py:229
+        x = flatten_nhwc(att_stats_pool(x, p.conv(), p.conv()))
+    else:
+        x = flatten_nhwc(stats_pool(x))
     return _head_tail(p, x)
 
 

@@ -46,6 +46,7 @@ CASES = [
     ("dpn68", 40, 64, 2),
     ("res2net50_w24_s4_c32", 80, 37, 2),       # odd T: ceil downsampling
     ("dpn68", 80, 33, 1),                      # odd T: SAME asymmetric pads
+    ("res2net101_w24_s4_c32_att", 40, 48, 2),  # attentive stats pooling (§8 f1)
 ]
 
 

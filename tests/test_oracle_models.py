@@ -11,21 +11,45 @@ import pytest
 from oracle import models_ref as R
 
 
-@pytest.mark.parametrize("name,F,T,N", [
-    ("tdnn", 40, 60, 3),
-    ("tdnn", 80, 33, 2),
-    ("res2net50_w8_s6_c16", 24, 40, 2),
-    ("res2net50_w24_s4_c32", 16, 29, 2),
-    ("dpn68", 16, 27, 2),
+@pytest.mark.parametrize("name,F,T,N,tol", [
+    ("tdnn", 40, 60, 3, 1e-4),
+    ("tdnn", 80, 33, 2, 1e-4),
+    ("res2net50_w8_s6_c16", 24, 40, 2, 1e-4),
+    ("res2net50_w24_s4_c32", 16, 29, 2, 1e-4),
+    ("dpn68", 16, 27, 2, 1e-4),
+    # 101 layers + attentive pooling: fp32 summation-order drift grows with depth
+    ("res2net101_w24_s4_c32_att", 16, 24, 2, 1e-3),
 ])
-def test_oracle_matches_torch(weights, name, F, T, N):
+def test_oracle_matches_torch(weights, name, F, T, N, tol):
     from voxsrc2020_speaker_verification_amd import synth
     spec, t, blob = weights(name, F)
     x = synth.make_features(N, T, F, seed=5)
     a = R.forward(spec, t, x)
     b = synth.torch_forward(spec, t, x)
     assert a.shape == (N, spec["output_dim"])
-    assert np.abs(a - b).max() <= 1e-4 * np.abs(b).max()
+    assert np.abs(a - b).max() <= tol * np.abs(b).max()
+
+
+def test_att_stats_pool_definition():
+    """models.py:273-303 restated by loops: logits from [x, mean, std] tiled
+    over time, softmax over time, sqrt(E_w[x^2] - E_w[x]^2 + eps)."""
+    rng = np.random.default_rng(3)
+    N, T, W, C, A = 2, 5, 3, 4, 6
+    x = rng.standard_normal((N, T, W, C)).astype(np.float32)
+    k1 = (rng.standard_normal((1, 1, 3 * C, A)) * 0.3).astype(np.float32)
+    k2 = (rng.standard_normal((1, 1, A, C)) * 0.3).astype(np.float32)
+    got = R.att_stats_pool(x, k1, k2)
+    for n in range(N):
+        for w in range(W):
+            xs = x[n, :, w, :].astype(np.float64)                  # [T, C]
+            mu, sd = xs.mean(0), np.sqrt(xs.var(0) + 1e-5)
+            a = np.concatenate([xs, np.tile(mu, (T, 1)), np.tile(sd, (T, 1))], 1)
+            lg = np.tanh(a @ k1[0, 0]) @ k2[0, 0]
+            wt = np.exp(lg - lg.max(0)) / np.exp(lg - lg.max(0)).sum(0)
+            m = (xs * wt).sum(0)
+            s = np.sqrt((xs * xs * wt).sum(0) - m * m + 1e-5)
+            np.testing.assert_allclose(got[n, 0, w, :C], m, rtol=1e-5, atol=1e-6)
+            np.testing.assert_allclose(got[n, 0, w, C:], s, rtol=1e-5, atol=1e-6)
 
 
 def test_tf_same_padding_rules():
@@ -94,7 +118,10 @@ def test_weight_blob_roundtrip_and_param_counts(weights):
     # README.md:190,241-262 parameter counts (code recount)
     counts = {("tdnn", 40): 3.51, ("res2net50_w24_s4_c32", 80): 17.73,
               ("res2net50_w24_s4_c64", 80): 32.07, ("res2net50_w8_s6_c16", 80): 4.78,
-              ("dpn68", 80): 15.97, ("dpn68", 40): 13.84}
+              ("dpn68", 80): 15.97, ("dpn68", 40): 13.84,
+              # code recount; README.md:245 rounds to 29.3 M (152/200 README values
+              # disagree with the code's block sizes)
+              ("res2net101_w24_s4_c32_att", 80): 29.17}
     for (name, F), m in counts.items():
         assert archs.param_count(archs.get_arch(name, F)) / 1e6 == pytest.approx(m, abs=0.006)
     with pytest.raises(ValueError):

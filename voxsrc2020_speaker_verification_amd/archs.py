@@ -50,6 +50,20 @@ ARCHS = {
                                 widths=[8, 16, 32, 64], block_sizes=[3, 4, 6, 3],
                                 block_strides=[1, 2, 2, 2], split=6, output_dim=192,
                                 expand_dim=3),
+    # res2net_model.py:264-280 -- deeper Res2Nets with attentive statistics
+    # pooling (models.py:273-303, att_dim 128, attention over [x, mean, std])
+    "res2net101_w24_s4_c32_att": dict(family="res2net", num_filters=[32, 64, 128, 256],
+                                      widths=[24, 48, 96, 192], block_sizes=[3, 4, 23, 3],
+                                      block_strides=[1, 2, 2, 2], split=4, output_dim=256,
+                                      expand_dim=3, pool="att", att_dim=128),
+    "res2net152_w24_s4_c32_att": dict(family="res2net", num_filters=[32, 64, 128, 256],
+                                      widths=[24, 48, 96, 192], block_sizes=[3, 8, 36, 3],
+                                      block_strides=[1, 2, 2, 2], split=4, output_dim=256,
+                                      expand_dim=3, pool="att", att_dim=128),
+    "res2net200_w24_s4_c32_att": dict(family="res2net", num_filters=[32, 64, 128, 256],
+                                      widths=[24, 48, 96, 192], block_sizes=[3, 24, 36, 3],
+                                      block_strides=[1, 2, 2, 2], split=4, output_dim=256,
+                                      expand_dim=3, pool="att", att_dim=128),
     # dpn_model.py:171 (num_init_features=10, k_r=128, G=32, k_sec, inc_sec)
     "dpn68": dict(family="dpn", num_init_features=10, k_r=128, bw=64, cardinality=32,
                   k_sec=[3, 4, 12, 3], inc_sec=[16, 32, 32, 64], output_dim=256,
@@ -165,6 +179,10 @@ def manifest(spec: dict):
                 _conv(out, namer, (1, 1, s * w, cout))  # conv1x1c :98
                 _bn(out, namer, cout)
                 cin = cout
+        if spec.get("pool") == "att":              # att_stats_pool, models.py:288-291
+            A = spec["att_dim"]
+            out.append(("att_stats_pool/conv2d/kernel", (1, 1, 3 * cin, A), "conv"))
+            out.append(("att_stats_pool/conv2d_1/kernel", (1, 1, A, cin), "conv"))
     elif fam == "dpn":
         G = spec["cardinality"]
         c0 = spec["num_init_features"]

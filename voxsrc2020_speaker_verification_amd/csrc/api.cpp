@@ -204,6 +204,8 @@ struct vox_model {
   std::vector<ConvW> convs;  // consumption order
   std::vector<BNW> bns;      // standalone BNs (prologues, pool BN, DPN final)
   ConvW head;                // dense as a 1x1 conv, fp32
+  bool att = false;          // attentive statistics pooling (models.py:273-303)
+  ConvW att_a, att_b, att_2; // fp32 1x1: W1[:C], W1[C:3C] (mean/std rows), W2
   BNW head_bn1;
   DevBuf slots[S_NSLOTS];
   size_t slot_need[S_NSLOTS] = {};
@@ -412,6 +414,22 @@ static int load_weights(vox_model* m, const std::vector<HostTensor>& ts) {
         if ((rc = conv_bn(m->eps4, c))) return rc;
         m->convs.push_back(c);
       }
+    if (m->spec.get("pool") == "att") {   // att_stats_pool kernels [1,1,3C,A], [1,1,A,C]
+      NEXT(k1, "attention kernel 1");
+      NEXT(k2, "attention kernel 2");
+      const int C3 = k1->shape[2], A = k1->shape[3], C = C3 / 3;
+      if (C3 != 3 * C || k2->shape[2] != A || k2->shape[3] != C)
+        return fail(VOX_EIO, "attention kernel shapes");
+      HostTensor ka = *k1, kb = *k1;
+      ka.shape = {1, 1, C, A};
+      ka.data.assign(k1->data.begin(), k1->data.begin() + (size_t)C * A);
+      kb.shape = {1, 1, 2 * C, A};
+      kb.data.assign(k1->data.begin() + (size_t)C * A, k1->data.end());
+      if ((rc = make_conv(m, ka, 1, nullptr, nullptr, 0.f, F32, m->att_a))) return rc;
+      if ((rc = make_conv(m, kb, 1, nullptr, nullptr, 0.f, F32, m->att_b))) return rc;
+      if ((rc = make_conv(m, *k2, 1, nullptr, nullptr, 0.f, F32, m->att_2))) return rc;
+      m->att = true;
+    }
   } else if (m->family == "dpn") {
     const int G = m->spec.geti("cardinality");
     ConvW stem;
@@ -599,6 +617,7 @@ static void emit_conv(Builder& B, const ConvW& cw, Act x, const void* x2, int ld
       }
     }
   }
+  if (dt_override == F32) op.type = 5;
   const double es = dt_override == F32 ? 4.0 : (double)es_of(B.m);
   op.flops = 2.0 * M * cw.cout * cw.groups * (double)cw.kh * cw.kw * cw.cin;
   op.bytes = es * ((double)x.N * x.H * x.W * cw.cin * cw.groups * (x2 ? 2 : 1) +
@@ -615,6 +634,63 @@ static void emit_pool(Builder& B, Act x, float* out, const BNW& bn) {
   op.inv = (const float*)bn.inv->p;
   op.out = out;
   op.bytes = (double)es_of(B.m) * x.N * x.H * x.W * x.C + 4.0 * x.N * x.W * 2 * x.C;
+  B.ops->push_back(op);
+}
+
+// Attentive statistics pooling (models.py:273-303) in fp32:
+//   S = [mean, std] over time              (stats-pool kernel, no BN)
+//   Bnw = S W1[C:3C]                        (fp32 1x1 over the N*W rows)
+//   H = tanh(x W1[:C] + Bnw)                (fp32 1x1 + bias/tanh kernel)
+//   L = H W2 ; softmax over time ; weighted mean/std ; head BN -> pooled
+static void emit_att_pool(Builder& B, Act x, float* pooled, Slot free_s) {
+  vox_model* m = B.m;
+  const int n = x.N, H = x.H, W = x.W, C = x.C, A = m->att_a.cout;
+  float* S = (float*)B.base(S_B, (size_t)n * W * 2 * C * 4);
+  float* bnw = (float*)B.base(S_PART, (size_t)n * W * A * 4);
+  float* hb = (float*)B.base(S_SC, (size_t)n * H * W * A * 4);
+  float* lg = (float*)B.base(free_s, (size_t)n * H * W * C * 4);
+  {
+    Op op;
+    op.kind = OP_POOL;
+    op.type = 2;
+    op.src = x.p; op.N = n; op.H = H; op.W = W; op.C = C;
+    op.mean = nullptr; op.inv = nullptr; op.out = S;
+    op.bytes = (double)es_of(m) * n * H * W * C + 4.0 * n * W * 2 * C;
+    B.ops->push_back(op);
+  }
+  emit_conv(B, m->att_b, Act{S, 2 * C, n * W, 1, 1, 2 * C}, nullptr, 0, 1, 1, 1, 1, 0, 0, 1, 1, bnw,
+            A, 0, nullptr, 0, nullptr, 0, 1 << 30, nullptr, nullptr, F32);
+  const float* x32 = (const float*)x.p;
+  if (m->dt == BF16) {
+    float* xc = (float*)B.base(S_A, (size_t)n * H * W * C * 4);
+    Op op;
+    op.kind = OP_OTHER;
+    op.type = 15;
+    op.src = x.p; op.dst = xc; op.count = (int64_t)n * H * W * C;
+    op.bytes = 6.0 * op.count;
+    B.ops->push_back(op);
+    x32 = xc;
+  }
+  emit_conv(B, m->att_a, Act{x32, C, n, H, W, C}, nullptr, 0, 1, 1, 1, 1, 0, 0, H, W, hb, A, 0,
+            nullptr, 0, nullptr, 0, 1 << 30, nullptr, nullptr, F32);
+  {
+    Op op;
+    op.kind = OP_OTHER;
+    op.type = 16;
+    op.dst = hb; op.src = bnw; op.N = n; op.H = H; op.W = W; op.C = A;
+    op.bytes = 8.0 * n * H * W * A;
+    B.ops->push_back(op);
+  }
+  emit_conv(B, m->att_2, Act{hb, A, n, H, W, A}, nullptr, 0, 1, 1, 1, 1, 0, 0, H, W, lg, C, 0,
+            nullptr, 0, nullptr, 0, 1 << 30, nullptr, nullptr, F32);
+  Op op;
+  op.kind = OP_POOL;
+  op.type = 17;
+  op.src = x.p; op.part = lg; op.N = n; op.H = H; op.W = W; op.C = C;
+  op.mean = (const float*)m->head_bn1.mean->p;
+  op.inv = (const float*)m->head_bn1.inv->p;
+  op.out = pooled;
+  op.bytes = (double)es_of(m) * n * H * W * C + 4.0 * n * H * W * C + 4.0 * n * W * 2 * C;
   B.ops->push_back(op);
 }
 
@@ -962,7 +1038,10 @@ static int build_res2net(Builder& B, const float* x, int n, int t, float* out) {
     }
   }
   float* pooled = (float*)B.base(S_POOL, (size_t)n * W * 2 * cur.C * 4);
-  emit_pool(B, cur, pooled, m->head_bn1);
+  if (m->att)
+    emit_att_pool(B, cur, pooled, nxt_s);
+  else
+    emit_pool(B, cur, pooled, m->head_bn1);
   emit_head(B, pooled, n, out);
   return VOX_OK;
 }
@@ -1084,6 +1163,11 @@ static hipError_t run_op(vox_model* m, const Op& op, hipStream_t s) {
     case 12: return launch_bneck(op.bq, op.cin, op.C, op.cl.wco, op.S, s);
     case 13: return launch_chain_rows(op.ch, s);
     case 14: return launch_split_s2(op.ch, s);
+    case 15: return launch_convert_bf16(op.src, (float*)op.dst, op.count, s);
+    case 16: return launch_att_bias_tanh((float*)op.dst, (const float*)op.src, op.N, op.H, op.W, op.C, s);
+    case 17:
+      return launch_att_pool(m->dt, op.src, op.part, op.N, op.H, op.W, op.C, 1e-5f, op.mean,
+                             op.inv, op.out, s);
     case 11:
       return launch_stem(m->dt, (const float*)op.src, op.N, op.H, op.W, op.part, op.C, op.mean,
                          op.inv, op.dst, s);
@@ -1307,7 +1391,8 @@ extern "C" int vox_plan_describe(vox_model* m, const float* d_x, int n, int t, i
   if ((rc = ensure_plan(m, d_x, n, t, (float*)m->stage_out.p))) return rc;
   std::string out;
   static const char* tn[] = {"igemm", "reduce", "pool", "avgpool", "convert", "igemm32", "bnrelu",
-                             "win", "rr", "gemm", "chain", "stem", "bneck", "chainrows", "splits2"};
+                             "win", "rr", "gemm", "chain", "stem", "bneck", "chainrows", "splits2",
+                             "cvt16", "atttanh", "attpool"};
   for (const Op& o : m->plan) {
     char line[256];
     const ConvParams& p = o.cp;

@@ -109,6 +109,14 @@ hipError_t launch_gemm1x1(const ConvParams& p, hipStream_t s);
 hipError_t launch_stem(DType t, const float* x, int N, int H, int W, const float* wts, int Cout,
                        const float* mean, const float* inv, void* y, hipStream_t s);
 int conv_kstep(DType t);   // 32 (bf16) / 16 (fp32)
+// Attentive statistics pooling glue (fp32): bf16 -> fp32 copy; h = tanh(h +
+// b[n][w]) over [N][H][W][A]; softmax-over-time weighted mean/std (+ optional
+// head BN) into the NHWC-flattened [N][W*2C] feature vector.
+hipError_t launch_convert_bf16(const void* x, float* y, int64_t n, hipStream_t s);
+hipError_t launch_att_bias_tanh(float* h, const float* b, int N, int H, int W, int A, hipStream_t s);
+hipError_t launch_att_pool(DType t, const void* x, const float* lg, int N, int H, int W, int C,
+                           float eps, const float* mean, const float* inv, float* out,
+                           hipStream_t s);
 int conv_vec(DType t);     // elements per 16-byte lane load: 8 / 4
 
 hipError_t launch_splitk_reduce(const float* partial, int S, int M, int coutp, int cout,

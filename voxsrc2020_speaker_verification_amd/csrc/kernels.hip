@@ -1512,3 +1512,90 @@ hipError_t launch_bnrelu_inplace(DType t, void* x, int ld, int64_t npix, int C, 
 }
 
 }  // namespace vox
+
+namespace vox {
+
+// ----------------------------------------------------------------------------
+// Attentive statistics pooling (models.py:273-303), fp32.  The attention MLP
+// runs as fp32 1x1 convs on the conv path; these kernels are the glue:
+//   conv1x1([x, tile(mean), tile(std)], W1) = x W1[:C] + [mean, std] W1[C:]
+// so the (time-invariant) second term is one small GEMM per (n, w) and is
+// added here before the tanh.
+__global__ void convert_bf16_f32_k(const bf16_t* __restrict__ x, float* __restrict__ y, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) y[i] = (float)x[i];
+}
+
+hipError_t launch_convert_bf16(const void* x, float* y, int64_t n, hipStream_t s) {
+  const int64_t blocks = (n + 255) / 256;
+  hipLaunchKernelGGL(convert_bf16_f32_k, dim3((unsigned)blocks), dim3(256), 0, s,
+                     reinterpret_cast<const bf16_t*>(x), y, n);
+  return hipGetLastError();
+}
+
+// h[n][t][w][a] = tanh(h + b[n][w][a])
+__global__ void att_bias_tanh_k(float* __restrict__ h, const float* __restrict__ b, int H, int W,
+                                int A, int64_t total) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int a = (int)(i % A);
+  const int64_t pix = i / A;
+  const int w = (int)(pix % W);
+  const int64_t n = pix / ((int64_t)H * W);
+  h[i] = tanhf(h[i] + b[(n * W + w) * A + a]);
+}
+
+hipError_t launch_att_bias_tanh(float* h, const float* b, int N, int H, int W, int A,
+                                hipStream_t s) {
+  const int64_t total = (int64_t)N * H * W * A;
+  hipLaunchKernelGGL(att_bias_tanh_k, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, h, b,
+                     H, W, A, total);
+  return hipGetLastError();
+}
+
+// Softmax over time of the logits, weighted mean and std of x, head BN, NHWC
+// flatten (feature w*2C + j).  One thread per (n, w, c): coalesced over c.
+template <typename T>
+__global__ void att_pool_k(const T* __restrict__ x, const float* __restrict__ lg, int N, int H,
+                           int W, int C, float eps, const float* __restrict__ mean,
+                           const float* __restrict__ inv, float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)N * W * C) return;
+  const int c = (int)(i % C);
+  const int64_t nw = i / C;
+  const int w = (int)(nw % W);
+  const int64_t n = nw / W;
+  const int64_t base = (n * H * W + w) * C + c, st = (int64_t)W * C;
+  float mx = -INFINITY;
+  for (int t = 0; t < H; ++t) mx = fmaxf(mx, lg[base + t * st]);
+  float sum = 0.f;
+  for (int t = 0; t < H; ++t) sum += expf(lg[base + t * st] - mx);
+  float wm = 0.f, wss = 0.f;
+  for (int t = 0; t < H; ++t) {
+    const float wt = expf(lg[base + t * st] - mx) / sum;
+    const float xv = (float)x[base + t * st];
+    wm += xv * wt;
+    wss += xv * xv * wt;
+  }
+  const float sd = sqrtf(wss - wm * wm + eps);
+  float* o = out + n * W * 2 * C + (int64_t)w * 2 * C;
+  const int j0 = w * 2 * C + c, j1 = j0 + C;
+  o[c] = mean ? (wm - mean[j0]) * inv[j0] : wm;
+  o[C + c] = mean ? (sd - mean[j1]) * inv[j1] : sd;
+}
+
+hipError_t launch_att_pool(DType t, const void* x, const float* lg, int N, int H, int W, int C,
+                           float eps, const float* mean, const float* inv, float* out,
+                           hipStream_t s) {
+  const int64_t total = (int64_t)N * W * C;
+  const dim3 grid((unsigned)((total + 255) / 256));
+  if (t == BF16)
+    hipLaunchKernelGGL((att_pool_k<bf16_t>), grid, dim3(256), 0, s,
+                       reinterpret_cast<const bf16_t*>(x), lg, N, H, W, C, eps, mean, inv, out);
+  else
+    hipLaunchKernelGGL((att_pool_k<float>), grid, dim3(256), 0, s,
+                       reinterpret_cast<const float*>(x), lg, N, H, W, C, eps, mean, inv, out);
+  return hipGetLastError();
+}
+
+}  // namespace vox

@@ -118,6 +118,21 @@ def _stats_pool(x, eps):
     return y.permute(0, 2, 3, 1).reshape(x.shape[0], -1)   # NHWC flatten
 
 
+def _att_stats_pool(x, k1, k2, eps):
+    """models.py:273-303 on NCHW: attention logits from [x, mean, std] (tiled
+    over T), softmax over T, weighted mean / std per (channel, frequency)."""
+    import torch
+    mean = x.mean(dim=2, keepdim=True)
+    var = ((x - mean) ** 2).mean(dim=2, keepdim=True)
+    ms = torch.cat([mean, torch.sqrt(var + eps)], dim=1).expand(-1, -1, x.shape[2], -1)
+    h = torch.tanh(_conv(torch.cat([x, ms], dim=1), k1))
+    w = torch.softmax(_conv(h, k2), dim=2)
+    wm = (x * w).sum(dim=2, keepdim=True)
+    wss = (x * x * w).sum(dim=2, keepdim=True)
+    y = torch.cat([wm, torch.sqrt(wss - wm * wm + eps)], dim=1)
+    return y.permute(0, 2, 3, 1).reshape(x.shape[0], -1)
+
+
 def torch_forward(spec, tensors, feats, calibrate=False):
     """Independent torch-CPU forward (fp32).  With calibrate=True the BN moving
     statistics in `tensors` are overwritten by batch statistics, in order."""
@@ -187,7 +202,10 @@ def torch_forward(spec, tensors, feats, calibrate=False):
             x = F.relu(p.bn(torch.cat(state, 1), e4))
         else:
             raise ValueError(fam)
-        x = _stats_pool(x, archs.STATS_POOL_EPS)
+        if spec.get("pool") == "att":
+            x = _att_stats_pool(x, p.conv(), p.conv(), archs.STATS_POOL_EPS)
+        else:
+            x = _stats_pool(x, archs.STATS_POOL_EPS)
         x = p.bn(x, e2)
         x = x @ p.conv()
         x = p.bn(x, e2)
