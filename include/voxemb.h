@@ -23,6 +23,7 @@
  *   vox_embed_utt             <- the chunk loop + length-weighted average
  *                                (tensorflow/tf_extract.py:96-111)
  *   vox_stats_pool_device     <- stats_pool (tensorflow/models/models.py:262-269)
+ *   vox_asnorm_stats          <- get_cohort_mean_std (tensorflow/snorm.py:83-109)
  *                                followed by the head's first BN
  *                                (res2net_model.py:239)
  *   vox_sliding_cmn           <- Kaldi `apply-cmvn-sliding --norm-vars=false
@@ -96,6 +97,14 @@ int vox_plan_describe(vox_model* m, const float* d_x, int n, int t, int f, char*
 int vox_stats_pool_device(const void* d_x, int dtype, int n, int h, int w, int c,
                           const float* d_mean, const float* d_inv, float* d_out,
                           void* stream);
+
+/* Adaptive s-norm cohort statistics (tensorflow/snorm.py:83-109,
+ * get_cohort_mean_std): for each trial row, the mean and population std of
+ * its top-k cosine scores against the cohort rows (callers l2-normalise both,
+ * as snorm.py does).  Device pointers: trial [n,d], cohort [m,d] float32,
+ * mean/std [n].  k = min(topk, m); d % 4 == 0.  Synchronises `stream`. */
+int vox_asnorm_stats(const float* d_trial, int n, const float* d_cohort, int m, int d,
+                     int topk, float* d_mean, float* d_std, void* stream);
 
 const char* vox_last_error(void);
 

@@ -44,6 +44,8 @@ _SIGS = [
                                     C.c_size_t]),
     ("vox_stats_pool_device", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
                                         C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, _P]),
+    ("vox_asnorm_stats", C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int,
+                                   C.c_void_p, C.c_void_p, C.c_void_p]),
     ("vox_last_error", C.c_char_p, []),
     ("vox_sliding_cmn", C.c_int, [_F, C.c_int, C.c_int, C.c_int, C.c_int, _F]),
     ("vox_mat_shape", C.c_int, [C.c_char_p, C.c_int64, C.POINTER(C.c_int), C.POINTER(C.c_int)]),

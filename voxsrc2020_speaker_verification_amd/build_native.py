@@ -15,6 +15,7 @@ ARCH = os.environ.get("VOX_OFFLOAD_ARCH", "gfx950")
 SOURCES = [
     ("kernels.hip", ["-O3"]),
     ("bneck.hip", ["-O3"]),
+    ("asnorm.hip", ["-O3"]),
     ("api.cpp", ["-O2"]),
     ("kaldi_host.cpp", ["-O2", "-ffp-contract=off"]),
 ]

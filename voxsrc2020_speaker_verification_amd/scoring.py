@@ -81,6 +81,31 @@ def cohort_mean_std(trial_xvectors, cohort, topk=400, block=1024):
     return mean_d, std_d
 
 
+def cohort_mean_std_gpu(trial_xvectors, cohort, topk=400, device=0):
+    """cohort_mean_std on the GPU (vox_asnorm_stats: fp32 MFMA score GEMM +
+    exact radix top-k select, libvoxemb).  Same inputs and outputs; scores
+    are summed in a different order than numpy's sgemm, so a trial whose k-th
+    and (k+1)-th cohort scores tie within float rounding may pick the other
+    member (the reference's own choice there is BLAS-dependent too)."""
+    import ctypes as C
+    import torch
+    from ._native import check, lib
+    utt = list(trial_xvectors)
+    trial = np.ascontiguousarray(np.array(list(trial_xvectors.values())), dtype=np.float32)
+    cmat = np.ascontiguousarray(np.array(list(cohort.values())), dtype=np.float32)
+    dev = torch.device("cuda", device)
+    td, cd = torch.from_numpy(trial).to(dev), torch.from_numpy(cmat).to(dev)
+    md = torch.empty(len(utt), dtype=torch.float32, device=dev)
+    sd = torch.empty_like(md)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    check(lib().vox_asnorm_stats(C.c_void_p(td.data_ptr()), trial.shape[0],
+                                 C.c_void_p(cd.data_ptr()), cmat.shape[0], trial.shape[1],
+                                 int(topk), C.c_void_p(md.data_ptr()), C.c_void_p(sd.data_ptr()),
+                                 C.c_void_p(stream)))
+    m, s = md.cpu().numpy(), sd.cpu().numpy()
+    return ({u: m[i] for i, u in enumerate(utt)}, {u: s[i] for i, u in enumerate(utt)})
+
+
 def cosine_scores(trial_xvectors, trial_path):
     scores = []
     with open(trial_path, "r") as f:

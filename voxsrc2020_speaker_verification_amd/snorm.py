@@ -24,6 +24,9 @@ def main(argv=None):
     ap.add_argument("--weight_matrix", type=str, default=None,
                     help="projection matrix as .npy (the reference's .pkl is not unpickled)")
     ap.add_argument("--snorm_score", type=str, default=None)
+    ap.add_argument("--gpu", type=int, default=None,
+                    help="device for the cohort top-k statistics (vox_asnorm_stats); "
+                         "default: numpy, exactly as snorm.py")
     a = ap.parse_args(argv)
     test = S.read_xvector(a.test_ark)
     if a.test_spk2utt is not None:
@@ -37,7 +40,10 @@ def main(argv=None):
             cohort = S.projection_cohort(np.load(a.weight_matrix, allow_pickle=False))
         else:
             raise ValueError("Can not compute snorm scores: no cohort vectors provided")
-        m, s = S.cohort_mean_std(test, cohort)
+        if a.gpu is None:
+            m, s = S.cohort_mean_std(test, cohort)
+        else:
+            m, s = S.cohort_mean_std_gpu(test, cohort, device=a.gpu)
         S.write_scores(a.snorm_score, S.asnorm_scores(m, s, cos))
     return 0
 
