@@ -55,6 +55,29 @@ def _kernel_name(tag, dt):
     return {1: "stats_pool_k", 2: "splitk_reduce", 3: "other"}.get(kind, "other")
 
 
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_summary.json")
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per dispatch of `kernel` from the committed rocprofv3 PMC
+    summary (tools/pmc_summary.py: FETCH_SIZE x2 + WRITE_SIZE, the gfx950
+    corrections of MI355X_MICROARCH.md "HBM"), averaged over the template
+    instances of the same kernel by dispatch count; None if not profiled."""
+    try:
+        with open(PMC_SUMMARY) as f:
+            summ = json.load(f)
+    except (OSError, ValueError):
+        return None
+    base = kernel.split("<")[0]
+    tot = disp = 0.0
+    for name, r in summ.items():
+        if name.split("::")[-1].split("<")[0] == base and "hbm_bytes" in r:
+            n = r["mean"].get("dispatches", 1)
+            tot += r["hbm_bytes"] * n
+            disp += n
+    return tot / disp if disp else None
+
+
 def weights_blob(model, feat_dim, cache_dir):
     from voxsrc2020_speaker_verification_amd import archs, synth, weights
     path = os.path.join(cache_dir, f"voxemb_{model}_{feat_dim}_seed1.blob")
@@ -192,7 +215,9 @@ def main():
     pool = groups.get("stats_pool_k")
     roof = {"bound": "mfma", "kernel": dom_name, "launches_per_step": dom["n"],
             "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
-            "frac": round(ach / peak, 4), "traffic": None,
+            "frac": round(ach / peak, 4), "traffic": pmc_traffic(dom_name),
+            "traffic_unit": "HBM bytes per launch (rocprofv3 PMC, profiles/pmc_summary.json)",
+            "algorithmic_bytes_per_launch": dom["bytes"] / dom["n"],
             "avg_launch_us": round(dom["ms"] / dom["n"] * 1e3, 2),
             "flop_per_launch": dom["flops"] / dom["n"]}
     extra = {
@@ -209,7 +234,8 @@ def main():
         gbs = pool["bytes"] / pool["n"] / (pool["ms"] / pool["n"] * 1e-3) / 1e9
         extra["stats_pool_roofline"] = {"bound": "hbm", "achieved": round(gbs, 1),
                                         "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                                        "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": None,
+                                        "frac": round(gbs / PEAK_HBM_GBS, 4),
+                                        "traffic": pmc_traffic("stats_pool_k"),
                                         "bytes_per_launch": pool["bytes"] / pool["n"]}
 
     cpu = None
