@@ -23,7 +23,10 @@ def weights_for(name, feat_dim, seed=1):
         import io
         from voxsrc2020_speaker_verification_amd import archs, synth, weights
         spec = archs.get_arch(name, feat_dim)
-        t = synth.make_weights(spec, seed=seed, calib_n=8, calib_T=120)
+        # Res2Nets: damped residual branches -> well-conditioned synthetic network,
+        # so bf16-vs-fp32 checks are meaningful (synth.make_weights docstring)
+        gain = 0.25 if spec["family"] == "res2net" else None
+        t = synth.make_weights(spec, seed=seed, calib_n=8, calib_T=120, residual_gain=gain)
         buf = io.BytesIO()
         weights.save_blob(buf, spec, t)
         _WEIGHTS[key] = (spec, t, buf.getvalue())

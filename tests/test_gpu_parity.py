@@ -5,8 +5,13 @@ Tolerances (north_star: "within 1e-3 relative on fp32"):
                 per-utterance cosine >= 0.999999.
   * bf16 mode:  bf16 activations / fp32 accumulation.  There is no bf16
                 reference; the bar is per-utterance cosine to the fp32 oracle
-                >= 0.99 and relative L2 error <= 0.15 (the EER delta it maps to
-                needs VoxCeleb data and a trained .pb).
+                >= 0.995 and relative L2 error <= 0.10, on well-conditioned
+                synthetic weights (Res2Net residual branches damped during BN
+                calibration, conftest/synth.make_weights: plain random-init
+                Res2Nets amplify any 1e-3 perturbation chaotically).  Observed:
+                cosine >= 0.9994 (Res2Net), 0.99999 (TDNN), 0.9976 (DPN68).
+                Bit-level bf16 checks are the kernel-variant equality tests below
+                and tests/test_bneck_unit.py.
 """
 
 import numpy as np
@@ -33,8 +38,9 @@ def _check_fp32(got, ref):
 def _check_bf16(got, ref):
     cos = _cos(got, ref)
     rel = np.linalg.norm(got - ref, axis=1) / np.linalg.norm(ref, axis=1)
-    assert cos.min() >= 0.99, f"bf16 cosine {cos.min():.5f}"
-    assert rel.max() <= 0.15, f"bf16 rel L2 {rel.max():.3f}"
+    print(f"bf16 cosine min {cos.min():.6f} rel L2 max {rel.max():.4f}")
+    assert cos.min() >= 0.995, f"bf16 cosine {cos.min():.5f}"
+    assert rel.max() <= 0.10, f"bf16 rel L2 {rel.max():.3f}"
 
 
 CASES = [

@@ -67,9 +67,10 @@ class _TorchParams:
         self.i += 1
         return self.torch.from_numpy(np.ascontiguousarray(self.tensors[name]))
 
-    def bn(self, x, eps):
+    def bn(self, x, eps, gain=None):
         """Inference BN; in calibration mode first set the moving stats to the
-        batch statistics of `x` (per channel over N,H,W; or over N for 2-D)."""
+        batch statistics of `x` (per channel over N,H,W; or over N for 2-D),
+        the variance divided by gain**2 when a gain is given."""
         torch = self.torch
         nm, nv = self.names[self.i], self.names[self.i + 1]
         self.i += 2
@@ -78,6 +79,8 @@ class _TorchParams:
             xd = x.double()
             m = xd.mean(dim=dims)
             v = ((xd - m.view((1, -1) + (1,) * (x.dim() - 2))) ** 2).mean(dim=dims)
+            if gain is not None:
+                v = v / (gain * gain)
             self.tensors[nm] = m.float().numpy()
             self.tensors[nv] = v.float().numpy()
         m = torch.from_numpy(self.tensors[nm])
@@ -133,9 +136,11 @@ def _att_stats_pool(x, k1, k2, eps):
     return y.permute(0, 2, 3, 1).reshape(x.shape[0], -1)
 
 
-def torch_forward(spec, tensors, feats, calibrate=False):
+def torch_forward(spec, tensors, feats, calibrate=False, residual_gain=None):
     """Independent torch-CPU forward (fp32).  With calibrate=True the BN moving
-    statistics in `tensors` are overwritten by batch statistics, in order."""
+    statistics in `tensors` are overwritten by batch statistics, in order;
+    residual_gain scales the calibrated Res2Net residual branches (the 1x1c
+    BN) so the synthetic network is well-conditioned (see make_weights)."""
     import torch
     import torch.nn.functional as F
     e4, e2 = archs.BN_EPS_4D, archs.BN_EPS_2D
@@ -178,7 +183,7 @@ def torch_forward(spec, tensors, feats, calibrate=False):
                     else:
                         outs.append(F.avg_pool2d(parts[s - 1], 3, st))
                     h = torch.cat(outs, dim=1)
-                    h = p.bn(_conv(h, p.conv()), e4)
+                    h = p.bn(_conv(h, p.conv()), e4, residual_gain)
                     x = F.relu(h + sc)
         elif fam == "dpn":
             G = spec["cardinality"]
@@ -213,9 +218,15 @@ def torch_forward(spec, tensors, feats, calibrate=False):
     return x.numpy()
 
 
-def make_weights(spec, seed=1, calib_n=16, calib_T=200, calib_seed=12345):
-    """Variance-scaling init + one BN calibration pass."""
+def make_weights(spec, seed=1, calib_n=16, calib_T=200, calib_seed=12345, residual_gain=None):
+    """Variance-scaling init + one BN calibration pass.
+
+    With plain calibration a random-init Res2Net is chaotic: an fp32 input
+    perturbation of 1e-3 already moves embeddings to cosine ~0.98, and bf16
+    rounding to ~0.85 (DESIGN.md "Precision").  residual_gain (e.g. 0.25)
+    damps every residual branch during calibration, giving a well-conditioned
+    network (as trained ones are) on which bf16-vs-fp32 checks discriminate."""
     t = init_weights(spec, seed)
     feats = make_features(calib_n, calib_T, spec["feat_dim"], calib_seed)
-    torch_forward(spec, t, feats, calibrate=True)
+    torch_forward(spec, t, feats, calibrate=True, residual_gain=residual_gain)
     return t
