@@ -185,9 +185,10 @@ def test_extract_cli_end_to_end(weights, tmp_path):
 
 
 @pytest.mark.parametrize("unfused_env", [("VOXEMB_NO_BNECK",), ("VOXEMB_NO_CHAIN_ROWS",),
-                                         ("VOXEMB_NO_SPLIT_S2",),
-                                         ("VOXEMB_NO_BNECK", "VOXEMB_NO_CHAIN", "VOXEMB_NO_SPLIT_S2")],
-                         ids=["chain", "tiled_chain", "split_s2", "unfused"])
+                                         ("VOXEMB_NO_SPLIT_S2",), ("VOXEMB_NO_GEMM_PIPE",),
+                                         ("VOXEMB_NO_BNECK", "VOXEMB_NO_CHAIN", "VOXEMB_NO_SPLIT_S2",
+                                          "VOXEMB_NO_GEMM_PIPE")],
+                         ids=["chain", "tiled_chain", "split_s2", "gemm_pipe", "unfused"])
 @pytest.mark.parametrize("name,F,T,N", [("res2net50_w24_s4_c32", 80, 200, 3),
                                         ("res2net50_w24_s4_c32", 80, 37, 3),
                                         ("res2net50_w24_s4_c32", 40, 75, 2),
@@ -206,6 +207,25 @@ def test_fused_kernels_bitwise_equal_unfused(weights, name, F, T, N, unfused_env
     with _extractor(blob, "bf16") as ex:
         unfused = ex.run(x)
     assert np.array_equal(fused, unfused)
+
+
+@pytest.mark.parametrize("N,T", [(16, 200), (7, 123)])
+def test_gemm_pipe_bitwise_many_tiles(weights, N, T, monkeypatch):
+    """The persistent pipelined GEMM (several tiles per workgroup, the load
+    stream crossing tile boundaries, ragged last pixel tile) gives the same
+    bits as the per-tile gemm1x1_lds."""
+    import torch
+    from voxsrc2020_speaker_verification_amd import synth
+    spec, t, blob = weights("res2net50_w24_s4_c32", 80)
+    x = synth.make_features(N, T, 80, seed=9)
+    with _extractor(blob, "bf16") as ex:
+        pipe = ex.run(x)
+        assert any(l.startswith("gemmpipe") for l in ex.describe(torch.from_numpy(x).cuda()))
+    monkeypatch.setenv("VOXEMB_NO_GEMM_PIPE", "1")
+    with _extractor(blob, "bf16") as ex:
+        ref = ex.run(x)
+        assert not any(l.startswith("gemmpipe") for l in ex.describe(torch.from_numpy(x).cuda()))
+    assert np.array_equal(pipe, ref)
 
 
 def test_bneck_segments_bitwise(weights, monkeypatch):

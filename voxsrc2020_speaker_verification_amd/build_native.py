@@ -16,6 +16,7 @@ SOURCES = [
     ("kernels.hip", ["-O3"]),
     ("bneck.hip", ["-O3"]),
     ("asnorm.hip", ["-O3"]),
+    ("gemm.hip", ["-O3"]),
     ("api.cpp", ["-O2"]),
     ("kaldi_host.cpp", ["-O2", "-ffp-contract=off"]),
 ]

@@ -221,6 +221,9 @@ struct vox_model {
   int win_cin = 0;             // VOXEMB_WIN_CIN=c: conv_win only for Cin == c (debug)
   bool no_rr = false;          // VOXEMB_NO_RR=1: disable conv1x1_rr
   bool no_gemm = false;        // VOXEMB_NO_GEMM=1: disable gemm1x1_lds
+  bool no_gemm_pipe = false;   // VOXEMB_NO_GEMM_PIPE=1: gemm1x1_lds instead of gemm1x1_pipe
+  int num_cu = 256;            // compute units (persistent grids)
+  int gemm_var = 0;            // VOXEMB_GEMM_VAR: gemm1x1_pipe variant (A/B experiments)
   int gemm_min_k = 192;        // VOXEMB_GEMM_MIN_K: smallest K routed to gemm1x1_lds (K=128 is faster on rr)
   bool no_chain = false;       // VOXEMB_NO_CHAIN=1: unfused Res2Net branches
   bool no_stem = false;        // VOXEMB_NO_STEM=1: stem through the generic conv
@@ -554,6 +557,8 @@ static void emit_conv(Builder& B, const ConvW& cw, Act x, const void* x2, int ld
         cw.cout >= 128 && 3 * (cout128 - cw.cout) <= cout128) {
       op.type = 9;
       p.coutp = cout128;
+      // persistent LDS-DMA pipelined GEMM (gemm.hip) where its tiling applies
+      if (!B.m->no_gemm_pipe && gemm_pipe_ok(p)) op.type = 18;
     }
   }
   // bf16 convs (stride 1 or 2) without prologue: window-staged LDS kernel if
@@ -1159,6 +1164,7 @@ static hipError_t run_op(vox_model* m, const Op& op, hipStream_t s) {
     case 7: return launch_conv_win(op.cp, op.cl, s);
     case 8: return launch_conv1x1_rr(op.cp, op.cl, s);
     case 9: return launch_gemm1x1(op.cp, s);
+    case 18: return launch_gemm_pipe(op.cp, m->num_cu, m->gemm_var, s);
     case 10: return launch_split_chain(op.ch, op.cl.wco, op.cl.wpx, s);
     case 12: return launch_bneck(op.bq, op.cin, op.C, op.cl.wco, op.S, s);
     case 13: return launch_chain_rows(op.ch, s);
@@ -1215,6 +1221,12 @@ extern "C" int vox_load_blob(const void* blob, size_t nbytes, int device, int pr
   HIPCHK(hipSetDevice(device));
   std::unique_ptr<vox_model> m(new vox_model());
   m->device = device;
+  {
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
+        ncu > 0)
+      m->num_cu = ncu;
+  }
   m->dt = precision == VOX_BF16 ? BF16 : F32;
   m->spec = spec;
   m->family = spec.get("family");
@@ -1227,6 +1239,8 @@ extern "C" int vox_load_blob(const void* blob, size_t nbytes, int device, int pr
   if (const char* e = std::getenv("VOXEMB_NO_RR")) m->no_rr = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_RR_WPX")) m->rr_wpx = std::atoi(e);
   if (const char* e = std::getenv("VOXEMB_NO_GEMM")) m->no_gemm = std::atoi(e) != 0;
+  if (const char* e = std::getenv("VOXEMB_NO_GEMM_PIPE")) m->no_gemm_pipe = std::atoi(e) != 0;
+  if (const char* e = std::getenv("VOXEMB_GEMM_VAR")) m->gemm_var = std::atoi(e);
   if (const char* e = std::getenv("VOXEMB_GEMM_MIN_K")) m->gemm_min_k = std::atoi(e);
   if (const char* e = std::getenv("VOXEMB_NO_CHAIN")) m->no_chain = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_NO_STEM")) m->no_stem = std::atoi(e) != 0;
@@ -1360,6 +1374,8 @@ extern "C" int vox_profile(vox_model* m, const float* d_x, int n, int t, int f, 
         tag |= (o.cl.wco << 4) | (o.cl.wpx << 8) | (1 << 15);
       else if (o.type == 9)
         tag |= (1 << 21);
+      else if (o.type == 18)
+        tag |= (1 << 27);
       else if (o.type == 10)
         tag |= (o.cl.wco << 4) | (o.cl.wpx << 8) | (1 << 22);
       else if (o.type == 11)
@@ -1392,11 +1408,11 @@ extern "C" int vox_plan_describe(vox_model* m, const float* d_x, int n, int t, i
   std::string out;
   static const char* tn[] = {"igemm", "reduce", "pool", "avgpool", "convert", "igemm32", "bnrelu",
                              "win", "rr", "gemm", "chain", "stem", "bneck", "chainrows", "splits2",
-                             "cvt16", "atttanh", "attpool"};
+                             "cvt16", "atttanh", "attpool", "gemmpipe"};
   for (const Op& o : m->plan) {
     char line[256];
     const ConvParams& p = o.cp;
-    if (o.type == 0 || o.type == 5 || o.type == 7 || o.type == 8 || o.type == 9)
+    if (o.type == 0 || o.type == 5 || o.type == 7 || o.type == 8 || o.type == 9 || o.type == 18)
       std::snprintf(line, sizeof(line),
                     "%s wco=%d wpx=%d s=%d N=%d H=%d W=%d Cin=%d Ho=%d Wo=%d Cout=%d k=%dx%d st=%d "
                     "g=%d flags=%d x2=%d pro=%d flops=%.4g bytes=%.4g\n",

@@ -104,6 +104,10 @@ int conv1x1_rr_max_wpx(int ks);
 // bf16 1x1 conv as an LDS-tiled GEMM (128x128 tile, BK 64): cinp % 64 == 0,
 // coutp % 128 == 0, paired-row weights, Cout/ysplit/ld multiples of 8.
 hipError_t launch_gemm1x1(const ConvParams& p, hipStream_t s);
+// Persistent LDS-DMA pipelined 1x1 GEMM (gemm.hip): 256-pixel x 128-cout tiles,
+// one workgroup per CU.  gemm_pipe_ok: K % 64 == 0, K >= 192, coutp % 128 == 0.
+int gemm_pipe_ok(const ConvParams& p);
+hipError_t launch_gemm_pipe(const ConvParams& p, int num_cu, int variant, hipStream_t s);
 // 1-input-channel 3x3 SAME stem + BN + ReLU from the fp32 features;
 // wts = [9][Cout] fp32 (bf16-rounded values in bf16 mode), Cout <= 64.
 hipError_t launch_stem(DType t, const float* x, int N, int H, int W, const float* wts, int Cout,
