@@ -17,6 +17,7 @@ SOURCES = [
     ("bneck.hip", ["-O3"]),
     ("asnorm.hip", ["-O3"]),
     ("gemm.hip", ["-O3"]),
+    ("gconv.hip", ["-O3"]),
     ("api.cpp", ["-O2"]),
     ("kaldi_host.cpp", ["-O2", "-ffp-contract=off"]),
 ]
@@ -37,7 +38,7 @@ def build(verbose=False, force=False) -> str:
     newest_hdr = max([os.path.getmtime(hdr), os.path.getmtime(__file__)] +
                      [os.path.getmtime(os.path.join(CSRC, n)) for n in os.listdir(CSRC)
                       if n.endswith(".h")])
-    objs, relink = [], force or not os.path.exists(LIB)
+    objs, relink, jobs = [], force or not os.path.exists(LIB), []
     for src, flags in SOURCES:
         path = os.path.join(CSRC, src)
         obj = os.path.join(outdir, src + ".o")
@@ -46,11 +47,18 @@ def build(verbose=False, force=False) -> str:
                 os.path.getmtime(obj) >= max(newest_hdr, os.path.getmtime(path))):
             continue
         lang = ["-x", "hip"] if src.endswith(".hip") else []
-        cmd = [hipcc, f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-c", *lang,
-               path, "-o", obj, *flags]
-        if verbose:
-            print(" ".join(cmd), file=sys.stderr)
-        subprocess.run(cmd, check=True)
+        jobs.append([hipcc, f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-c", *lang,
+                     path, "-o", obj, *flags])
+    if jobs:
+        from concurrent.futures import ThreadPoolExecutor
+
+        def _cc(cmd):
+            if verbose:
+                print(" ".join(cmd), file=sys.stderr)
+            subprocess.run(cmd, check=True)
+
+        with ThreadPoolExecutor(max_workers=min(len(jobs), 6)) as pool:
+            list(pool.map(_cc, jobs))
         relink = True
     if not relink and all(os.path.getmtime(LIB) >= os.path.getmtime(o) for o in objs):
         return LIB

@@ -157,6 +157,7 @@ struct ConvW {
   std::shared_ptr<DevBuf> wtc;       // bf16 [coutp][taps*cin] for conv_win (groups == 1)
   std::shared_ptr<DevBuf> wpair;     // bf16 [coutp][kp] paired-row layout for conv1x1_rr
   std::shared_ptr<DevBuf> wstem;     // fp32 [9][cout] for the 1-channel 3x3 stem kernel
+  std::shared_ptr<DevBuf> wgc;       // bf16 [C/16][NM][64][8] expanded grouped 3x3 (gconv.hip)
   std::shared_ptr<DevBuf> mean, inv; // optional epilogue BN (cout*groups)
 };
 
@@ -189,6 +190,7 @@ struct Op {
   int64_t count = 0;
   ChainParams ch{};
   BneckParams bq{};  // type 12: Cin (cin), C, w (cl.wco), split (S)
+  GconvParams gq{};  // type 19
   int cin = 0;
   double flops = 0, bytes = 0;
 };
@@ -222,6 +224,7 @@ struct vox_model {
   bool no_rr = false;          // VOXEMB_NO_RR=1: disable conv1x1_rr
   bool no_gemm = false;        // VOXEMB_NO_GEMM=1: disable gemm1x1_lds
   bool no_gemm_pipe = false;   // VOXEMB_NO_GEMM_PIPE=1: gemm1x1_lds instead of gemm1x1_pipe
+  bool no_gconv = false;       // VOXEMB_NO_GCONV=1: grouped 3x3 on the generic implicit GEMM
   int num_cu = 256;            // compute units (persistent grids)
   int gemm_var = 0;            // VOXEMB_GEMM_VAR: gemm1x1_pipe variant (A/B experiments)
   int gemm_min_k = 192;        // VOXEMB_GEMM_MIN_K: smallest K routed to gemm1x1_lds (K=128 is faster on rr)
@@ -296,6 +299,36 @@ static int make_conv(vox_model* m, const HostTensor& k, int groups, const HostTe
     out.wpair = std::make_shared<DevBuf>();
     HIPCHK(out.wpair->ensure(h.size() * 2));
     HIPCHK(hipMemcpy(out.wpair->p, h.data(), h.size() * 2, hipMemcpyHostToDevice));
+  }
+  if (dt == BF16 && groups > 1 && kh == 3 && kw == 3 && cin == cout &&
+      (cin == 4 || cin == 8 || cin == 16 || cin == 32) && (cout * groups) % 64 == 0) {
+    // gconv.hip A fragments: slab sg = output channels [16sg, 16sg+16), MFMA m,
+    // lane l -> row co = 16sg + (l & 15), k-group q = l >> 4, element e:
+    //   gw 32: tap m, input channel 8q+e of the group;
+    //   gw <= 16: tap 2m + (q>>1) (tap 9 = zero), input channel 16sg + 8(q&1) + e,
+    //             zero unless it lies in co's group (block-diagonal)
+    const int gw = cin, C = cout * groups, NM = gw == 32 ? 9 : 5;
+    std::vector<uint16_t> h((size_t)C / 16 * NM * 64 * 8, 0);
+    for (int sg = 0; sg < C / 16; ++sg)
+      for (int mm = 0; mm < NM; ++mm)
+        for (int l = 0; l < 64; ++l)
+          for (int e = 0; e < 8; ++e) {
+            const int co = 16 * sg + (l & 15), q = l >> 4;
+            int tap, ci;
+            if (gw == 32) {
+              tap = mm;
+              ci = 32 * (co / 32) + 8 * q + e;
+            } else {
+              tap = 2 * mm + (q >> 1);
+              ci = 16 * sg + 8 * (q & 1) + e;
+            }
+            if (tap >= 9 || ci / gw != co / gw) continue;
+            h[(((size_t)sg * NM + mm) * 64 + l) * 8 + e] =
+                f2bf(k.data[((size_t)tap * cin + ci % gw) * cout_all + col0 + co]);
+          }
+    out.wgc = std::make_shared<DevBuf>();
+    HIPCHK(out.wgc->ensure(h.size() * 2));
+    HIPCHK(hipMemcpy(out.wgc->p, h.data(), h.size() * 2, hipMemcpyHostToDevice));
   }
   if (groups == 1 && cin == 1 && kh == 3 && kw == 3 && cout <= 64) {
     std::vector<float> h(9 * (size_t)cout);
@@ -1104,9 +1137,31 @@ static int build_dpn(Builder& B, const float* x, int n, int t, float* out) {
       const BNW& b2 = m->bns[bi++];
       const ConvW& c2 = m->convs[ci++];
       char* Bb = B.base(S_B, (size_t)n * Ho * Wo * r * es);
-      emit_conv(B, c2, Act{A, r, n, Hi, Wi, r}, nullptr, 0, bs, bs, 1, 1, tf_same_beg(Hi, 3, bs),
-                tf_same_beg(Wi, 3, bs), Ho, Wo, Bb, r, 0, nullptr, 0, nullptr, 0, 1 << 30,
-                (const float*)b2.mean->p, (const float*)b2.inv->p);
+      GconvParams g{};
+      g.x = A; g.ldx = r; g.in_mean = (const float*)b2.mean->p; g.in_inv = (const float*)b2.inv->p;
+      g.w = c2.wgc ? c2.wgc->p : nullptr; g.y = Bb; g.ldy = r;
+      g.N = n; g.H = Hi; g.W = Wi; g.C = r; g.Ho = Ho; g.Wo = Wo; g.gw = c2.cin;
+      g.sh = bs; g.ph = tf_same_beg(Hi, 3, bs); g.pw = tf_same_beg(Wi, 3, bs);
+      if (c2.wgc && !m->no_gconv && c2.cin * c2.groups == r && gconv_ok(g)) {
+        // row segments: enough workgroups to cover the chip a few times over,
+        // each segment >= 4 steps (warm-up window re-read per segment)
+        const int rs = gconv_rs(g);
+        int nseg = 1;
+        while ((long)n * (r / 64) * nseg < 2048 && Ho / (2 * nseg) >= 4 * rs) nseg *= 2;
+        g.seg = (Ho + nseg - 1) / nseg;
+        g.nseg = (Ho + g.seg - 1) / g.seg;
+        Op op;
+        op.kind = OP_CONV;
+        op.type = 19;
+        op.gq = g;
+        op.flops = 2.0 * n * Ho * Wo * (double)r * 9.0 * c2.cin;
+        op.bytes = es * ((double)n * Hi * Wi * r + (double)n * Ho * Wo * r);
+        B.ops->push_back(op);
+      } else {
+        emit_conv(B, c2, Act{A, r, n, Hi, Wi, r}, nullptr, 0, bs, bs, 1, 1, tf_same_beg(Hi, 3, bs),
+                  tf_same_beg(Wi, 3, bs), Ho, Wo, Bb, r, 0, nullptr, 0, nullptr, 0, 1 << 30,
+                  (const float*)b2.mean->p, (const float*)b2.inv->p);
+      }
       // 1x1c -> [res add in place | new dense channels appended]
       const BNW& b3 = m->bns[bi++];
       const ConvW& c3 = m->convs[ci++];
@@ -1165,6 +1220,7 @@ static hipError_t run_op(vox_model* m, const Op& op, hipStream_t s) {
     case 8: return launch_conv1x1_rr(op.cp, op.cl, s);
     case 9: return launch_gemm1x1(op.cp, s);
     case 18: return launch_gemm_pipe(op.cp, m->num_cu, m->gemm_var, s);
+    case 19: return launch_gconv(op.gq, s);
     case 10: return launch_split_chain(op.ch, op.cl.wco, op.cl.wpx, s);
     case 12: return launch_bneck(op.bq, op.cin, op.C, op.cl.wco, op.S, s);
     case 13: return launch_chain_rows(op.ch, s);
@@ -1240,6 +1296,7 @@ extern "C" int vox_load_blob(const void* blob, size_t nbytes, int device, int pr
   if (const char* e = std::getenv("VOXEMB_RR_WPX")) m->rr_wpx = std::atoi(e);
   if (const char* e = std::getenv("VOXEMB_NO_GEMM")) m->no_gemm = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_NO_GEMM_PIPE")) m->no_gemm_pipe = std::atoi(e) != 0;
+  if (const char* e = std::getenv("VOXEMB_NO_GCONV")) m->no_gconv = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_GEMM_VAR")) m->gemm_var = std::atoi(e);
   if (const char* e = std::getenv("VOXEMB_GEMM_MIN_K")) m->gemm_min_k = std::atoi(e);
   if (const char* e = std::getenv("VOXEMB_NO_CHAIN")) m->no_chain = std::atoi(e) != 0;
@@ -1386,6 +1443,8 @@ extern "C" int vox_profile(vox_model* m, const float* d_x, int n, int t, int f, 
         tag |= (1 << 25);
       else if (o.type == 14)
         tag |= (1 << 26);
+      else if (o.type == 19)
+        tag |= (1 << 28);
       else if (o.type == 8)
         tag |= (o.cl.wco << 4) | (o.cl.wpx << 8) | (((o.cp.cinp + 31) / 32) << 16) | (1 << 20);
       else if (o.type == 0 || o.type == 5)
@@ -1408,7 +1467,7 @@ extern "C" int vox_plan_describe(vox_model* m, const float* d_x, int n, int t, i
   std::string out;
   static const char* tn[] = {"igemm", "reduce", "pool", "avgpool", "convert", "igemm32", "bnrelu",
                              "win", "rr", "gemm", "chain", "stem", "bneck", "chainrows", "splits2",
-                             "cvt16", "atttanh", "attpool", "gemmpipe"};
+                             "cvt16", "atttanh", "attpool", "gemmpipe", "gconv"};
   for (const Op& o : m->plan) {
     char line[256];
     const ConvParams& p = o.cp;
@@ -1423,6 +1482,10 @@ extern "C" int vox_plan_describe(vox_model* m, const float* d_x, int n, int t, i
       std::snprintf(line, sizeof(line), "bneck N=%d H=%d W=%d Cin=%d C=%d w=%d split=%d seg=%d nseg=%d flops=%.4g bytes=%.4g\n",
                     o.bq.N, o.bq.H, o.bq.W, o.cin, o.C, o.cl.wco, o.S, o.bq.seg, o.bq.nseg, o.flops,
                     o.bytes);
+    else if (o.type == 19)
+      std::snprintf(line, sizeof(line), "gconv N=%d H=%d W=%d C=%d gw=%d Ho=%d Wo=%d st=%d rs=%d seg=%d nseg=%d flops=%.4g bytes=%.4g\n",
+                    o.gq.N, o.gq.H, o.gq.W, o.gq.C, o.gq.gw, o.gq.Ho, o.gq.Wo, o.gq.sh,
+                    gconv_rs(o.gq), o.gq.seg, o.gq.nseg, o.flops, o.bytes);
     else if (o.type == 14)
       std::snprintf(line, sizeof(line), "splits2 N=%d H=%d W=%d w=%d nst=%d seg=%d nseg=%d lds=%d flops=%.4g bytes=%.4g\n",
                     o.ch.N, o.ch.H, o.ch.W, o.ch.w, o.ch.nst, o.ch.R, o.ch.nwaves, o.ch.lds,

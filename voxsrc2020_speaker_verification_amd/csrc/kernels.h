@@ -123,6 +123,25 @@ hipError_t launch_att_pool(DType t, const void* x, const float* lg, int N, int H
                            hipStream_t s);
 int conv_vec(DType t);     // elements per 16-byte lane load: 8 / 4
 
+// Row-streamed grouped 3x3 conv + BN/ReLU input prologue (gconv.hip), DPN
+// cardinality-32 convs: group width gw in {4,8,16,32}, C % 64 == 0, stride 1
+// (SAME) or 2 (TF SAME, pad-begin ph/pw in {0,1}), Wo <= 80.  Weights
+// expanded to [C/16][NM][64][8] bf16 (NM = 9 for gw 32, else 5; see gconv.hip).
+// Grid: N * nseg workgroups x C/64 chunks; `seg` output rows per segment.
+struct GconvParams {
+  const void* x; int ldx;
+  const float* in_mean; const float* in_inv;   // prologue relu((x-m)*inv) or null
+  const void* w;
+  void* y; int ldy;
+  int N, H, W, C, Ho, Wo, gw;
+  int sh, ph, pw;
+  int seg, nseg;
+};
+int gconv_ok(const GconvParams& p);
+int gconv_rs(const GconvParams& p);
+int gconv_lds(const GconvParams& p);
+hipError_t launch_gconv(const GconvParams& p, hipStream_t s);
+
 hipError_t launch_splitk_reduce(const float* partial, int S, int M, int coutp, int cout,
                                 const float* mean, const float* inv, int flags,
                                 float* out, int ldo, hipStream_t s);
