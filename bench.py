@@ -32,6 +32,8 @@ PEAK_HBM_GBS = 8000.0       # HBM3E spec
 
 def _kernel_name(tag, dt):
     kind = tag & 15
+    if tag & (1 << 29):
+        return "conv3x3_pipe"
     if tag & (1 << 28):
         return "gconv3x3_rows"
     if tag & (1 << 27):

@@ -228,6 +228,30 @@ def test_gemm_pipe_bitwise_many_tiles(weights, N, T, monkeypatch):
     assert np.array_equal(pipe, ref)
 
 
+@pytest.mark.parametrize("name,F,T,N", [("res2net50_w24_s4_c32", 80, 200, 4),
+                                        ("res2net50_w24_s4_c32", 80, 37, 3),
+                                        ("res2net50_w24_s4_c32", 40, 75, 2),
+                                        ("res2net50_w24_s4_c64", 40, 48, 2)])
+def test_conv3_pipe_bitwise_generic(weights, name, F, T, N, monkeypatch):
+    """The pipelined 3x3 implicit GEMM for the w = 96 / 192 branches (gathered
+    LDS-DMA operands, several tiles per workgroup, ragged pixel tiles, the
+    next branch's addend x_{k+1} + y_k formed in its epilogue in place) gives
+    the same bits as the generic implicit-GEMM conv that adds y_{k-1} on load."""
+    import torch
+    from voxsrc2020_speaker_verification_amd import synth
+    spec, t, blob = weights(name, F)
+    x = synth.make_features(N, T, F, seed=13)
+    with _extractor(blob, "bf16") as ex:
+        got = ex.run(x)
+        assert sum(l.startswith("conv3pipe") for l in ex.describe(torch.from_numpy(x).cuda())) >= 6
+    monkeypatch.setenv("VOXEMB_NO_CONV3", "1")
+    monkeypatch.setenv("VOXEMB_NO_WIN", "1")
+    with _extractor(blob, "bf16") as ex:
+        ref = ex.run(x)
+        assert not any(l.startswith("conv3pipe") for l in ex.describe(torch.from_numpy(x).cuda()))
+    assert np.array_equal(got, ref)
+
+
 def test_bneck_segments_bitwise(weights, monkeypatch):
     """Row segmentation of the fused bottleneck (N=1 -> many segments, warm-up
     rows recomputed) gives the same bits as one segment per utterance."""

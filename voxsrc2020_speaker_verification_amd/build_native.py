@@ -18,6 +18,7 @@ SOURCES = [
     ("asnorm.hip", ["-O3"]),
     ("gemm.hip", ["-O3"]),
     ("gconv.hip", ["-O3"]),
+    ("conv3.hip", ["-O3"]),
     ("api.cpp", ["-O2"]),
     ("kaldi_host.cpp", ["-O2", "-ffp-contract=off"]),
 ]

@@ -225,6 +225,7 @@ struct vox_model {
   bool no_gemm = false;        // VOXEMB_NO_GEMM=1: disable gemm1x1_lds
   bool no_gemm_pipe = false;   // VOXEMB_NO_GEMM_PIPE=1: gemm1x1_lds instead of gemm1x1_pipe
   bool no_gconv = false;       // VOXEMB_NO_GCONV=1: grouped 3x3 on the generic implicit GEMM
+  bool no_conv3 = false;       // VOXEMB_NO_CONV3=1: Res2Net w>=96 3x3 branches on conv_win/igemm
   int num_cu = 256;            // compute units (persistent grids)
   int gemm_var = 0;            // VOXEMB_GEMM_VAR: gemm1x1_pipe variant (A/B experiments)
   int gemm_min_k = 192;        // VOXEMB_GEMM_MIN_K: smallest K routed to gemm1x1_lds (K=128 is faster on rr)
@@ -1044,6 +1045,42 @@ static int build_res2net(Builder& B, const float* x, int n, int t, float* out) {
           chained = pooled = true;
         }
       }
+      if (!chained && m->dt == BF16 && !m->no_conv3) {
+        // wide branches (w = 96 / 192) on the pipelined 3x3 implicit GEMM
+        // (conv3.hip); at stride 1 branch j's epilogue also forms the next
+        // branch's input z_{j+1} = x_{j+1} + y_j in place over x_{j+1}
+        std::vector<Op> ops3;
+        bool ok = true;
+        for (int j = 0; ok && j < s - 1; ++j) {
+          const ConvW& br = m->convs[ci + j];
+          const bool z = stride == 1 && j < s - 2;
+          Op op;
+          op.kind = OP_CONV;
+          op.type = 20;
+          ConvParams& p = op.cp;
+          p.x = A ? A + (size_t)j * w * es : nullptr; p.ldx = sw;
+          p.w = br.wtc ? br.wtc->p : nullptr; p.kp = 9 * br.cin;
+          p.y = Bc ? Bc + (size_t)j * w * es : nullptr; p.ldy = sw;
+          p.res = (z && A) ? A + (size_t)(j + 1) * w * es : nullptr; p.ldr = sw;
+          p.y2 = (void*)p.res; p.ldy2 = sw; p.ysplit = 1 << 30;
+          p.mean = br.mean ? (const float*)br.mean->p : nullptr;
+          p.inv = br.inv ? (const float*)br.inv->p : nullptr;
+          p.N = n; p.H = H; p.W = W; p.Cin = br.cin; p.Ho = Ho; p.Wo = Wo;
+          p.Cout = br.cout; p.coutp = br.coutp;
+          p.kh = br.kh; p.kw = br.kw; p.sh = p.sw = stride; p.dh = p.dw = 1; p.ph = p.pw = 1;
+          p.groups = br.groups; p.flags = EPI_AFFINE | EPI_RELU;
+          ok = br.wtc && br.mean && br.cin == w && br.cout == w && conv3_pipe_ok(p);
+          op.flops = 2.0 * n * Ho * Wo * 9.0 * br.cin * br.cout;
+          op.bytes = (double)es * ((double)n * H * W * br.cin +
+                                   (double)n * Ho * Wo * br.cout * (z ? 3.0 : 1.0));
+          ops3.push_back(op);
+        }
+        if (ok) {
+          for (const Op& op : ops3) B.ops->push_back(op);
+          ci += s - 1;
+          chained = true;
+        }
+      }
       for (int j = 0; !chained && j < s - 1; ++j) {  // res2net_pad_conv_bn_relu :53-75
         const ConvW& br = m->convs[ci++];
         Act xin{A ? A + (size_t)j * w * es : nullptr, sw, n, H, W, w};
@@ -1221,6 +1258,7 @@ static hipError_t run_op(vox_model* m, const Op& op, hipStream_t s) {
     case 9: return launch_gemm1x1(op.cp, s);
     case 18: return launch_gemm_pipe(op.cp, m->num_cu, m->gemm_var, s);
     case 19: return launch_gconv(op.gq, s);
+    case 20: return launch_conv3_pipe(op.cp, m->num_cu, s);
     case 10: return launch_split_chain(op.ch, op.cl.wco, op.cl.wpx, s);
     case 12: return launch_bneck(op.bq, op.cin, op.C, op.cl.wco, op.S, s);
     case 13: return launch_chain_rows(op.ch, s);
@@ -1297,6 +1335,7 @@ extern "C" int vox_load_blob(const void* blob, size_t nbytes, int device, int pr
   if (const char* e = std::getenv("VOXEMB_NO_GEMM")) m->no_gemm = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_NO_GEMM_PIPE")) m->no_gemm_pipe = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_NO_GCONV")) m->no_gconv = std::atoi(e) != 0;
+  if (const char* e = std::getenv("VOXEMB_NO_CONV3")) m->no_conv3 = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_GEMM_VAR")) m->gemm_var = std::atoi(e);
   if (const char* e = std::getenv("VOXEMB_GEMM_MIN_K")) m->gemm_min_k = std::atoi(e);
   if (const char* e = std::getenv("VOXEMB_NO_CHAIN")) m->no_chain = std::atoi(e) != 0;
@@ -1445,6 +1484,8 @@ extern "C" int vox_profile(vox_model* m, const float* d_x, int n, int t, int f, 
         tag |= (1 << 26);
       else if (o.type == 19)
         tag |= (1 << 28);
+      else if (o.type == 20)
+        tag |= (1 << 29);
       else if (o.type == 8)
         tag |= (o.cl.wco << 4) | (o.cl.wpx << 8) | (((o.cp.cinp + 31) / 32) << 16) | (1 << 20);
       else if (o.type == 0 || o.type == 5)
@@ -1467,11 +1508,12 @@ extern "C" int vox_plan_describe(vox_model* m, const float* d_x, int n, int t, i
   std::string out;
   static const char* tn[] = {"igemm", "reduce", "pool", "avgpool", "convert", "igemm32", "bnrelu",
                              "win", "rr", "gemm", "chain", "stem", "bneck", "chainrows", "splits2",
-                             "cvt16", "atttanh", "attpool", "gemmpipe", "gconv"};
+                             "cvt16", "atttanh", "attpool", "gemmpipe", "gconv", "conv3pipe"};
   for (const Op& o : m->plan) {
     char line[256];
     const ConvParams& p = o.cp;
-    if (o.type == 0 || o.type == 5 || o.type == 7 || o.type == 8 || o.type == 9 || o.type == 18)
+    if (o.type == 0 || o.type == 5 || o.type == 7 || o.type == 8 || o.type == 9 || o.type == 18 ||
+        o.type == 20)
       std::snprintf(line, sizeof(line),
                     "%s wco=%d wpx=%d s=%d N=%d H=%d W=%d Cin=%d Ho=%d Wo=%d Cout=%d k=%dx%d st=%d "
                     "g=%d flags=%d x2=%d pro=%d flops=%.4g bytes=%.4g\n",

@@ -198,21 +198,37 @@ void gemm1x1_pipe(ConvParams p) {
   }
   const int swa = SWZ ? (col >> 1) & 7 : 0;   // (r>>1)&7 for every fragment row (rows differ by multiples of 16)
 
+  // epilogue operands (BN, residual tile) are fetched right after the DMA
+  // issue of step L0 = KT-1-LEAD, so LEAD steps of MFMAs cover their latency
+  // (K >= 192: KT >= 3)
+  constexpr int LEAD = 2;
+  const int L0 = KT - 1 - LEAD;
+  const int EPI_LD = ((flags & EPI_AFFINE) ? 8 : 0) + ((flags & EPI_RES) ? 8 : 0);
+  u32x4 rv[2][4];
+  u32x4 bm[2][2], bi[2][2];
   for (int s = 0; s < S; ++s) {
-    // operands of step s landed (this wave's DMA); younger: step s+1's six
-    // pieces plus, in the two steps after an epilogue, its eight stores
-    // (issued after step s's DMA when the epilogue ran at step s-1 or s-2)
-    if (epi_age <= 1) wait_vm<GP_NL + 8>(); else wait_vm<GP_NL>();
+    // operands of step s landed (this wave's DMA); younger: exactly the ops
+    // issued after that DMA -- step s+1's six pieces, the epilogue loads while
+    // in flight (steps L0+1 .. KT-1), and in the two steps after an epilogue
+    // its eight stores
+    const bool el = c_k > L0 && EPI_LD > 0;
+    if (epi_age <= 1) {
+      if (!el) wait_vm<GP_NL + 8>();
+      else if (EPI_LD == 16) wait_vm<GP_NL + 8 + 16>();
+      else wait_vm<GP_NL + 8 + 8>();
+    } else {
+      if (!el) wait_vm<GP_NL>();
+      else if (EPI_LD == 16) wait_vm<GP_NL + 16>();
+      else wait_vm<GP_NL + 8>();
+    }
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     const bool last = (c_k == KT - 1);
     const int lid = t_first + c_tile * t_step;
     const int co0 = (lid % cblocks) * GP_BN;
     const int px0 = (lid / cblocks) * GP_BM;
-    u32x4 rv[2][4];
-    u32x4 bm[2][2], bi[2][2];
-    if (last) {
-      // epilogue operands first: they land under this step's MFMAs
+    issue((s + 2) % GP_NST);
+    if (c_k == L0) {
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const int ch = co0 + wm * 64 + 32 * q + 8 * g;
@@ -232,7 +248,6 @@ void gemm1x1_pipe(ConvParams p) {
         }
       }
     }
-    issue((s + 2) % GP_NST);
     __builtin_amdgcn_sched_barrier(0);
     const int sb = (s % GP_NST) * GP_SLOT;
     const char* L = smem + sb;
@@ -252,7 +267,7 @@ void gemm1x1_pipe(ConvParams p) {
     }
     ++epi_age;
     if (last) {
-      // epilogue loads are older than step s+2's DMA: six younger ops remain.
+      // the epilogue loads precede LEAD DMA issues (steps L0+1 .. KT-1).
       // The wait names every asm-load destination, so nothing reads (or
       // copies) those registers before the data has landed.
       asm volatile("s_waitcnt vmcnt(%16)"
@@ -260,7 +275,7 @@ void gemm1x1_pipe(ConvParams p) {
                      "+v"(rv[1][0]), "+v"(rv[1][1]), "+v"(rv[1][2]), "+v"(rv[1][3]),
                      "+v"(bm[0][0]), "+v"(bm[0][1]), "+v"(bm[1][0]), "+v"(bm[1][1]),
                      "+v"(bi[0][0]), "+v"(bi[0][1]), "+v"(bi[1][0]), "+v"(bi[1][1])
-                   : "n"(GP_NL)
+                   : "n"(GP_NL * LEAD)
                    : "memory");
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll

@@ -108,6 +108,12 @@ hipError_t launch_gemm1x1(const ConvParams& p, hipStream_t s);
 // one workgroup per CU.  gemm_pipe_ok: K % 64 == 0, K >= 192, coutp % 128 == 0.
 int gemm_pipe_ok(const ConvParams& p);
 hipError_t launch_gemm_pipe(const ConvParams& p, int num_cu, int variant, hipStream_t s);
+// Persistent LDS-DMA pipelined 3x3 implicit GEMM (conv3.hip) for the Res2Net
+// branch convs with Cin in {96, 192}: stride 1 (SAME) or 2 (fixed pad 1),
+// Cout % 96 == 0, epilogue BN + ReLU; with y2 set (stride 1) it also writes
+// z = bf16(res + y) to y2 (the next branch's input, in place over res).
+int conv3_pipe_ok(const ConvParams& p);
+hipError_t launch_conv3_pipe(const ConvParams& p, int num_cu, hipStream_t s);
 // 1-input-channel 3x3 SAME stem + BN + ReLU from the fp32 features;
 // wts = [9][Cout] fp32 (bf16-rounded values in bf16 mode), Cout <= 64.
 hipError_t launch_stem(DType t, const float* x, int N, int H, int W, const float* wts, int Cout,
