@@ -225,7 +225,8 @@ struct vox_model {
   bool no_gemm = false;        // VOXEMB_NO_GEMM=1: disable gemm1x1_lds
   bool no_gemm_pipe = false;   // VOXEMB_NO_GEMM_PIPE=1: gemm1x1_lds instead of gemm1x1_pipe
   bool no_gconv = false;       // VOXEMB_NO_GCONV=1: grouped 3x3 on the generic implicit GEMM
-  bool no_conv3 = false;       // VOXEMB_NO_CONV3=1: Res2Net w>=96 3x3 branches on conv_win/igemm
+  bool no_conv3 = false;
+  bool no_gemm_pro = false;    // VOXEMB_NO_GEMM_PRO=1: prologue 1x1 convs off the pipelined GEMM       // VOXEMB_NO_CONV3=1: Res2Net w>=96 3x3 branches on conv_win/igemm
   int num_cu = 256;            // compute units (persistent grids)
   int gemm_var = 0;            // VOXEMB_GEMM_VAR: gemm1x1_pipe variant (A/B experiments)
   int gemm_min_k = 192;        // VOXEMB_GEMM_MIN_K: smallest K routed to gemm1x1_lds (K=128 is faster on rr)
@@ -593,6 +594,24 @@ static void emit_conv(Builder& B, const ConvW& cw, Act x, const void* x2, int ld
       p.coutp = cout128;
       // persistent LDS-DMA pipelined GEMM (gemm.hip) where its tiling applies
       if (!B.m->no_gemm_pipe && gemm_pipe_ok(p)) op.type = 18;
+    }
+  }
+  // bf16 1x1 with a BN+ReLU input prologue (DPN bn_relu_conv): the pipelined
+  // GEMM applies the prologue to its pixel fragments (gemm1x1_pipe<.., PRO>)
+  if (op.type != 18 && B.m->dt == BF16 && dt_override != F32 && in_mean && cw.wpair &&
+      !B.m->no_gemm_pipe && !B.m->no_gemm_pro && !(flags & EPI_PARTIAL) && ph == 0 && pw == 0 &&
+      cw.kh == 1 && cw.kw == 1 && cw.groups == 1 && cw.cout % 8 == 0 && ldy % 8 == 0 &&
+      (ysplit >= (1 << 30) || (ysplit % 8 == 0 && ldy2 % 8 == 0)) && (!res || ldr % 8 == 0) &&
+      x.ld % 8 == 0 && cw.kp <= x.ld) {
+    const int cout128 = (cw.cout + 127) / 128 * 128;
+    if (cw.cout >= 128 && 3 * (cout128 - cw.cout) <= cout128) {
+      ConvParams q = p;
+      q.coutp = cout128;
+      q.w = cw.wpair->p;
+      if (gemm_pipe_ok(q)) {
+        p = q;
+        op.type = 18;
+      }
     }
   }
   // bf16 convs (stride 1 or 2) without prologue: window-staged LDS kernel if
@@ -1336,6 +1355,7 @@ extern "C" int vox_load_blob(const void* blob, size_t nbytes, int device, int pr
   if (const char* e = std::getenv("VOXEMB_NO_GEMM_PIPE")) m->no_gemm_pipe = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_NO_GCONV")) m->no_gconv = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_NO_CONV3")) m->no_conv3 = std::atoi(e) != 0;
+  if (const char* e = std::getenv("VOXEMB_NO_GEMM_PRO")) m->no_gemm_pro = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_GEMM_VAR")) m->gemm_var = std::atoi(e);
   if (const char* e = std::getenv("VOXEMB_GEMM_MIN_K")) m->gemm_min_k = std::atoi(e);
   if (const char* e = std::getenv("VOXEMB_NO_CHAIN")) m->no_chain = std::atoi(e) != 0;

@@ -49,6 +49,7 @@ constexpr int GP_NL = GP_NA + GP_NB;       // DMA instructions per wave per step
 }  // namespace
 
 __device__ uint4 g_gemm_sink[64];          // destination of masked lanes' stores
+__device__ uint4 g_gemm_zero[4] = {};      // DMA source of the K tail past kp (PRO)
 
 __device__ __forceinline__ void glds16(const void* src, uint32_t lds) {
   unsigned keep;
@@ -83,7 +84,12 @@ template <int N> __device__ __forceinline__ void wait_vm() {
 }
 
 #pragma clang fp contract(off)
-template <int SWZ>
+// PRO: BN+ReLU input prologue relu((x - in_mean[k]) * in_inv[k]) applied to
+// the pixel fragments after their LDS read, with the prologue table staged
+// in LDS once (DPN68 bn_relu_conv, dpn_model.py:40-54); channels k >= Cin are
+// zero, as in the generic conv.  K may then end on a half step (kp % 64 = 32):
+// the tail DMA reads a zero line and the all-zero MFMA half step is skipped.
+template <int SWZ, bool PRO>
 __global__ __launch_bounds__(GP_NT) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void gemm1x1_pipe(ConvParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -94,7 +100,7 @@ void gemm1x1_pipe(ConvParams p) {
   const int col = lane & 15, g = lane >> 4;
   const int M = p.N * p.Ho * p.Wo;
   const int HoWo = p.Ho * p.Wo;
-  const int KT = p.kp / 64;
+  const int KT = (p.kp + 63) / 64;
   const int cblocks = p.coutp / GP_BN;
   const int T = ((M + GP_BM - 1) / GP_BM) * cblocks;
   // tiles of this workgroup: XCD x (blocks x, x+8, ...) owns the contiguous
@@ -126,6 +132,9 @@ void gemm1x1_pipe(ConvParams p) {
   // holds source chunk (tid%8) ^ ((r>>1)&7); rows 0..127 weights, 128.. pixels
   const int slot = tid & 7;
   const int rsub = tid >> 3;
+  // source chunk of every DMA piece of this thread (see set_load_tile)
+  const int cch = SWZ ? slot ^ ((rsub >> 1) & 7) : slot;
+  const bf16_t* gzero = reinterpret_cast<const bf16_t*>(g_gemm_zero);
   const uint32_t lds_wave = lds0 + (uint32_t)wave * 1024u;
 
   // load-side state: the tile whose operands are being fetched
@@ -156,10 +165,11 @@ void gemm1x1_pipe(ConvParams p) {
   auto issue = [&](int s_slot) {
     const uint32_t base = lds_wave + (uint32_t)s_slot * GP_SLOT;
     const int ko = l_k * 64;
+    const bool kin = !PRO || ko + cch * 8 < p.kp;
 #pragma unroll
-    for (int i = 0; i < GP_NA; ++i) glds16(pa[i] + ko, base + i * 8192u);
+    for (int i = 0; i < GP_NA; ++i) glds16(kin ? pa[i] + ko : gzero, base + i * 8192u);
 #pragma unroll
-    for (int i = 0; i < GP_NB; ++i) glds16(pb[i] + ko, base + (GP_NA + i) * 8192u);
+    for (int i = 0; i < GP_NB; ++i) glds16(kin ? pb[i] + ko : gzero, base + (GP_NA + i) * 8192u);
     // advance; past the last tile the final step is re-read (never consumed)
     if (l_k + 1 < KT) {
       ++l_k;
@@ -169,6 +179,16 @@ void gemm1x1_pipe(ConvParams p) {
       set_load_tile(l_tile);
     }
   };
+
+  const float* ptab = reinterpret_cast<const float*>(smem + GP_NST * GP_SLOT);
+  if (PRO) {
+    float* tab = reinterpret_cast<float*>(smem + GP_NST * GP_SLOT);
+    for (int k = tid; k < p.kp; k += GP_NT) {
+      tab[k] = k < p.Cin ? p.in_mean[k] : 0.f;
+      tab[p.kp + k] = k < p.Cin ? p.in_inv[k] : 0.f;
+    }
+    __syncthreads();   // no DMA in flight yet
+  }
 
   set_load_tile(0);
   issue(0);
@@ -253,12 +273,34 @@ void gemm1x1_pipe(ConvParams p) {
     const char* L = smem + sb;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
+      if (PRO && ks == 1 && last && (p.kp & 63)) break;   // zero half step past kp
       const int cs = ((ks * 4 + g) ^ swa) << 4;
       bf16x8 a[4], b[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         a[i] = *reinterpret_cast<const bf16x8*>(L + offa[i] + cs);
         b[i] = *reinterpret_cast<const bf16x8*>(L + offb[i] + cs);
+      }
+      if (PRO) {
+        // this lane group's 8 input channels of the step; bf16(relu((x-m)*inv))
+        const int kb = c_k * 64 + ks * 32 + 8 * g;
+        if (kb < p.Cin) {
+          const f32x4 m0 = *reinterpret_cast<const f32x4*>(ptab + kb);
+          const f32x4 m1 = *reinterpret_cast<const f32x4*>(ptab + kb + 4);
+          const f32x4 i0 = *reinterpret_cast<const f32x4*>(ptab + p.kp + kb);
+          const f32x4 i1 = *reinterpret_cast<const f32x4*>(ptab + p.kp + kb + 4);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              b[i][e] = (bf16_t)fmaxf(((float)b[i][e] - m0[e]) * i0[e], 0.f);
+              b[i][4 + e] = (bf16_t)fmaxf(((float)b[i][4 + e] - m1[e]) * i1[e], 0.f);
+            }
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) b[i] = bf16x8{};
+        }
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -308,7 +350,7 @@ void gemm1x1_pipe(ConvParams p) {
               v[4 + e] = (v[4 + e] - m1[e]) * i1[e];
             }
           }
-          if (flags & EPI_RES) {
+          if ((flags & EPI_RES) && ch < p.ysplit) {   // the dual-destination part has none
             const bf16x8 r8 = __builtin_bit_cast(bf16x8, rv[q][j]);
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] += (float)r8[e];
@@ -348,7 +390,15 @@ void gemm1x1_pipe(ConvParams p) {
 int gemm_pipe_ok(const ConvParams& p) {
   const int M = p.N * p.Ho * p.Wo;
   const int T = ((M + GP_BM - 1) / GP_BM) * (p.coutp / GP_BN);
-  return p.kp % 64 == 0 && p.kp / 64 >= 3 && p.coutp % GP_BN == 0 && T >= 8;
+  if (p.in_mean) {
+    // prologue variant: K in 32-steps, at least three 64-steps, table in LDS
+    if (p.kp % 32 || (p.kp + 63) / 64 < 3 || p.kp > 1024 || p.Cin > p.kp || p.Cin % 8 ||
+        !p.in_inv)
+      return 0;
+  } else if (p.kp % 64 || p.kp / 64 < 3) {
+    return 0;
+  }
+  return p.coutp % GP_BN == 0 && T >= 8;
 }
 
 hipError_t launch_gemm_pipe(const ConvParams& p, int num_cu, int variant, hipStream_t s) {
@@ -357,10 +407,13 @@ hipError_t launch_gemm_pipe(const ConvParams& p, int num_cu, int variant, hipStr
   const int T = ((M + GP_BM - 1) / GP_BM) * (p.coutp / GP_BN);
   int G = num_cu < T ? num_cu : T;
   G = G / 8 * 8;
-  if (variant == 1)
-    hipLaunchKernelGGL(gemm1x1_pipe<0>, dim3(G), dim3(GP_NT), GP_NST * GP_SLOT, s, p);
+  if (p.in_mean)
+    hipLaunchKernelGGL((gemm1x1_pipe<1, true>), dim3(G), dim3(GP_NT),
+                       GP_NST * GP_SLOT + 8 * p.kp, s, p);
+  else if (variant == 1)
+    hipLaunchKernelGGL((gemm1x1_pipe<0, false>), dim3(G), dim3(GP_NT), GP_NST * GP_SLOT, s, p);
   else
-    hipLaunchKernelGGL(gemm1x1_pipe<1>, dim3(G), dim3(GP_NT), GP_NST * GP_SLOT, s, p);
+    hipLaunchKernelGGL((gemm1x1_pipe<1, false>), dim3(G), dim3(GP_NT), GP_NST * GP_SLOT, s, p);
   return hipGetLastError();
 }
 
