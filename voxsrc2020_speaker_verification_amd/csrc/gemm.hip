@@ -84,11 +84,12 @@ template <int N> __device__ __forceinline__ void wait_vm() {
 }
 
 #pragma clang fp contract(off)
-// PRO: BN+ReLU input prologue relu((x - in_mean[k]) * in_inv[k]) applied to
-// the pixel fragments after their LDS read, with the prologue table staged
-// in LDS once (DPN68 bn_relu_conv, dpn_model.py:40-54); channels k >= Cin are
-// zero, as in the generic conv.  K may then end on a half step (kp % 64 = 32):
-// the tail DMA reads a zero line and the all-zero MFMA half step is skipped.
+// PRO: BN+ReLU input prologue relu((x - in_mean[k]) * in_inv[k]) (DPN68
+// bn_relu_conv, dpn_model.py:40-54), applied once per element to each step's
+// pixel rows in LDS after the DMA lands (prologue table staged in LDS at
+// start, one extra barrier per step); channels k >= Cin are zero, as in the
+// generic conv.  K may end on a half step (kp % 64 = 32): the tail DMA reads
+// a zero line and the all-zero MFMA half step is skipped.
 template <int SWZ, bool PRO>
 __global__ __launch_bounds__(GP_NT) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void gemm1x1_pipe(ConvParams p) {
@@ -243,6 +244,39 @@ void gemm1x1_pipe(ConvParams p) {
     }
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
+    if (PRO) {
+      // prologue once per element, in place in this step's LDS pixel rows:
+      // chunk (row r, slot sl) holds input channels k .. k+7 of the step,
+      // bf16(relu((x - m) * inv)), zero for k >= Cin (and for the zero tail)
+      char* Lw = smem + (s % GP_NST) * GP_SLOT;
+#pragma unroll
+      for (int i = 0; i < (GP_BM * 8) / GP_NT; ++i) {
+        const int chunk = tid + GP_NT * i;
+        const int r = chunk >> 3, sl = chunk & 7;
+        const int src = SWZ ? sl ^ ((r >> 1) & 7) : sl;
+        const int k = c_k * 64 + src * 8;
+        bf16x8* q = reinterpret_cast<bf16x8*>(Lw + (GP_BN + r) * 128 + sl * 16);
+        bf16x8 v = *q;
+        if (k < p.Cin) {
+          const f32x4 m0 = *reinterpret_cast<const f32x4*>(ptab + k);
+          const f32x4 m1 = *reinterpret_cast<const f32x4*>(ptab + k + 4);
+          const f32x4 i0 = *reinterpret_cast<const f32x4*>(ptab + p.kp + k);
+          const f32x4 i1 = *reinterpret_cast<const f32x4*>(ptab + p.kp + k + 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[e] = (bf16_t)fmaxf(((float)v[e] - m0[e]) * i0[e], 0.f);
+            v[4 + e] = (bf16_t)fmaxf(((float)v[4 + e] - m1[e]) * i1[e], 0.f);
+          }
+        } else {
+          v = bf16x8{};
+        }
+        *q = v;
+      }
+      // LDS writes visible to every wave; the DMA stays in flight (no vmcnt)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
     const bool last = (c_k == KT - 1);
     const int lid = t_first + c_tile * t_step;
     const int co0 = (lid % cblocks) * GP_BN;
@@ -280,27 +314,6 @@ void gemm1x1_pipe(ConvParams p) {
       for (int i = 0; i < 4; ++i) {
         a[i] = *reinterpret_cast<const bf16x8*>(L + offa[i] + cs);
         b[i] = *reinterpret_cast<const bf16x8*>(L + offb[i] + cs);
-      }
-      if (PRO) {
-        // this lane group's 8 input channels of the step; bf16(relu((x-m)*inv))
-        const int kb = c_k * 64 + ks * 32 + 8 * g;
-        if (kb < p.Cin) {
-          const f32x4 m0 = *reinterpret_cast<const f32x4*>(ptab + kb);
-          const f32x4 m1 = *reinterpret_cast<const f32x4*>(ptab + kb + 4);
-          const f32x4 i0 = *reinterpret_cast<const f32x4*>(ptab + p.kp + kb);
-          const f32x4 i1 = *reinterpret_cast<const f32x4*>(ptab + p.kp + kb + 4);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              b[i][e] = (bf16_t)fmaxf(((float)b[i][e] - m0[e]) * i0[e], 0.f);
-              b[i][4 + e] = (bf16_t)fmaxf(((float)b[i][4 + e] - m1[e]) * i1[e], 0.f);
-            }
-          }
-        } else {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) b[i] = bf16x8{};
-        }
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
