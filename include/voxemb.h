@@ -118,6 +118,13 @@ int vox_read_mat(const char* path, int64_t offset, float* out, int rows, int col
 int vox_parse_mat(const uint8_t* buf, size_t nbytes, float* out, int rows, int cols,
                   size_t* consumed);
 int vox_parse_mat_shape(const uint8_t* buf, size_t nbytes, int* rows, int* cols);
+/* The same two readers with CM payloads decoded in Kaldi C++'s arithmetic
+ * (CompressedMatrix::Uint16ToFloat / CharToFloat) instead of kaldi_io's: what
+ * the reference's `apply-cmvn-sliding ark:...` pipe (tf_extract.py:63) decodes
+ * from the `copy-feats --compress` arks (prepare_data.sh:69).  FM/DM: identical. */
+int vox_read_mat_kaldi(const char* path, int64_t offset, float* out, int rows, int cols);
+int vox_parse_mat_kaldi(const uint8_t* buf, size_t nbytes, float* out, int rows, int cols,
+                        size_t* consumed);
 /* Serialise "key \0BFV \4<u32 dim><dim f32>" into buf; returns bytes written
  * (or needed, if cap is too small) and the offset of "\0B" via *data_offset. */
 int64_t vox_format_vec_flt(const char* key, const float* v, int dim, uint8_t* buf,

@@ -67,3 +67,33 @@ def test_dp_extract_gloo(tmp_path, world, n_utts):
         np.testing.assert_array_equal(got[k], e)
     coh = np.load(tmp_path / "xvector.cohort.npy")
     assert coh.shape == (3, 8)
+
+
+def _failing_worker(rank, world, port, outdir):
+    import torch.distributed as dist
+    from voxsrc2020_speaker_verification_amd import dp_extract
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    rng = np.random.default_rng(rank)
+    # rank 1 holds a 10-frame utterance: the chunk rule divides by zero there
+    L = 10 if rank == 1 else 40
+    feats = [(f"u{rank}", rng.standard_normal((L, 4)).astype(np.float32))]
+    try:
+        dp_extract.run(rank, world, lambda r, w: feats, _fake_embed, 8, None, batch=3)
+        res = "ok"
+    except ZeroDivisionError:
+        res = "own"
+    except RuntimeError as e:
+        res = "peer" if "rank(s) [1]" in str(e) else repr(e)
+    with open(os.path.join(outdir, f"r{rank}"), "w") as f:
+        f.write(res)
+    dist.destroy_process_group()
+
+
+def test_dp_extract_rank_failure_aborts_all(tmp_path):
+    """A failing shard makes every rank abort before the gathers (no hang)."""
+    import torch.multiprocessing as mp
+    world = 3
+    mp.spawn(_failing_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    got = [open(tmp_path / f"r{r}").read() for r in range(world)]
+    assert got == ["peer", "own", "peer"]

@@ -84,6 +84,21 @@ def test_batch_independence(weights, precision):
             assert np.array_equal(one[0], full[i])
 
 
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_batch_independence_large_batch(weights, precision):
+    """Past 64 rows (several head row blocks) on the headline model: the head's
+    split-K partition is fixed per model, so embeddings stay bitwise equal."""
+    from voxsrc2020_speaker_verification_amd import synth
+    spec, t, blob = weights("res2net50_w24_s4_c32", 80)
+    x = synth.make_features(70, 32, 80, seed=11)
+    with _extractor(blob, precision) as ex:
+        full = ex.run(x)
+        part = ex.run(x[60:70])
+        one = ex.run(x[67:68])
+    assert np.array_equal(part, full[60:70])
+    assert np.array_equal(one[0], full[67])
+
+
 def test_chunk_rule_matches_oracle(weights):
     """tf_extract.py:96-111 on T=2030 (1000 + 1000 + 30) and T=1010 (tail dropped)."""
     from oracle import models_ref

@@ -39,6 +39,28 @@ def test_read_mat_ark_bit_exact(name):
         assert np.array_equal(got[k].view(np.uint32), exp[k].astype(np.float32).view(np.uint32)), k
 
 
+def test_read_mat_ark_cm_kaldi_cpp_order():
+    """cm="kaldi": Kaldi C++ CompressedMatrix arithmetic (the values the
+    reference's apply-cmvn-sliding pipe decodes), bit-exact vs the oracle's
+    restatement; within a few float32 ULPs of kaldi_io's order."""
+    from oracle import kaldi_ref
+    from voxsrc2020_speaker_verification_amd.kaldi import read_mat_ark
+    raw = open(os.path.join(G, "cm_mats.ark"), "rb").read()
+    exp_io = np.load(os.path.join(G, "cm_mats.npz"))
+    got = dict(read_mat_ark(os.path.join(G, "cm_mats.ark"), cm="kaldi"))
+    assert sorted(got) == sorted(exp_io.files)
+    ndiff = 0
+    for k in exp_io.files:
+        pos = raw.index(k.encode() + b" \0BCM ") + len(k) + 6
+        ref = kaldi_ref.cm_decode_kaldi(raw[pos:])
+        assert np.array_equal(got[k].view(np.uint32), ref.view(np.uint32)), k
+        io = exp_io[k].astype(np.float32)
+        np.testing.assert_allclose(got[k], io, rtol=4e-7, atol=4e-7 * np.abs(io).max())
+        ndiff += int((got[k] != io).sum())
+    # the two orders are genuinely different arithmetic on these fixtures
+    assert ndiff > 0
+
+
 def test_scp_offsets_and_ranges(tmp_path):
     """scp 'path:offset' lines point at '\\0B' (copy-vector ark,scp); matrix
     ranges [a:b,c:d] are inclusive as Kaldi's."""

@@ -52,6 +52,9 @@ _SIGS = [
     ("vox_read_mat", C.c_int, [C.c_char_p, C.c_int64, _F, C.c_int, C.c_int]),
     ("vox_parse_mat", C.c_int, [C.c_char_p, C.c_size_t, _F, C.c_int, C.c_int,
                                 C.POINTER(C.c_size_t)]),
+    ("vox_read_mat_kaldi", C.c_int, [C.c_char_p, C.c_int64, _F, C.c_int, C.c_int]),
+    ("vox_parse_mat_kaldi", C.c_int, [C.c_char_p, C.c_size_t, _F, C.c_int, C.c_int,
+                                      C.POINTER(C.c_size_t)]),
     ("vox_parse_mat_shape", C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(C.c_int),
                                       C.POINTER(C.c_int)]),
     ("vox_format_vec_flt", C.c_int64, [C.c_char_p, _F, C.c_int, C.c_void_p, C.c_size_t,

@@ -756,9 +756,11 @@ static void emit_head(Builder& B, const float* pooled, int n, float* out) {
   vox_model* m = B.m;
   const ConvW& hw = m->head;
   const int D = hw.cin;
-  // split-K: aim for ~512 blocks of 64 rows x 128 couts
-  const int gx = (n + 63) / 64, gy = hw.coutp / (16 * hw.wco);
-  int S = std::max(1, std::min(64, 512 / std::max(1, gx * gy)));
+  // split-K over a partition fixed per model (never per batch size n), so an
+  // utterance's fp32 partial sums -- and its embedding bits -- do not depend on
+  // its batch mates: ~256 K-slices x cout blocks (one 64-row block per slice)
+  const int gy = hw.coutp / (16 * hw.wco);
+  int S = std::max(1, std::min(64, 256 / std::max(1, gy)));
   int kchunk = (hw.cinp + S - 1) / S;
   kchunk = (kchunk + 15) / 16 * 16;
   S = (hw.cinp + kchunk - 1) / kchunk;

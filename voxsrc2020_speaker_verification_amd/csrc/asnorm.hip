@@ -120,6 +120,21 @@ extern "C" int vox_asnorm_stats(const float* d_trial, int n, const float* d_coho
     return vox_set_error(VOX_EINVAL, "bad asnorm arguments");
   if (d % 4) return vox_set_error(VOX_EINVAL, "embedding dim must be a multiple of 4");
   hipStream_t s = (hipStream_t)stream;
+  // the buffers and kernels go to the device that holds the trial matrix (the
+  // caller's stream belongs to it), not to this thread's current device
+  int dev = -1, prev = -1;
+  {
+    hipPointerAttribute_t at, ac;
+    if (hipPointerGetAttributes(&at, d_trial) != hipSuccess ||
+        hipPointerGetAttributes(&ac, d_cohort) != hipSuccess || at.type != hipMemoryTypeDevice ||
+        ac.type != hipMemoryTypeDevice)
+      return vox_set_error(VOX_EINVAL, "asnorm operands must be device memory");
+    if (at.device != ac.device)
+      return vox_set_error(VOX_EINVAL, "asnorm trial and cohort matrices on different devices");
+    dev = at.device;
+  }
+  if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(dev) != hipSuccess)
+    return vox_set_error(VOX_EHIP, "asnorm: cannot select the operands' device");
   const int k = topk < m ? topk : m;
   // cohort as fp32 1x1-conv weights [coutp][kp] (zero-padded rows / columns)
   const int KS = conv_kstep(F32);
@@ -160,5 +175,6 @@ extern "C" int vox_asnorm_stats(const float* d_trial, int n, const float* d_coho
 done:
   if (wbuf) (void)hipFree(wbuf);
   if (sbuf) (void)hipFree(sbuf);
+  (void)hipSetDevice(prev);
   return rc;
 }

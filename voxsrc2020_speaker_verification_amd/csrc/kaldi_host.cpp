@@ -6,7 +6,10 @@
 //     [t-w/2, t-w/2+w) shifted to stay inside [0,T), output = x - sum/n.
 //   * binary matrix reader "\0B" + FM / DM / CM (kaldi_io.py:420-454), with
 //     CM decoded exactly as kaldi_io._read_compressed_mat (kaldi_io.py:471-504,
-//     float32 arithmetic in the same operation order).
+//     float32 arithmetic in the same operation order: vox_read_mat), or with
+//     Kaldi C++'s CompressedMatrix arithmetic (vox_read_mat_kaldi: the values
+//     `apply-cmvn-sliding` sees when it reads the `copy-feats --compress` arks
+//     of prepare_data.sh:69).
 //   * FV record writer (kaldi_io.write_vec_flt, kaldi_io.py:304-334).
 // Compiled with -ffp-contract=off so no multiply-add is fused.
 #include <algorithm>
@@ -108,7 +111,13 @@ int parse_header(Reader& r, int* rows, int* cols, int* kind /*0 FM 1 DM 2 CM*/) 
   return VOX_OK;
 }
 
-int parse_payload(Reader& r, int kind, int rows, int cols, float* out) {
+// cm_kaldi = 0: kaldi_io._read_compressed_mat's float32 order (kaldi_io.py:471-504);
+// cm_kaldi = 1: Kaldi C++ CompressedMatrix (compressed-matrix.cc, what
+// `apply-cmvn-sliding` decodes in the reference pipeline, tf_extract.py:63):
+//   Uint16ToFloat = min + range * 1.52590218966964e-05f * v       (float, left to right)
+//   CharToFloat   = p + (q - p) * v * (1/64.0 | 1/128.0 | 1/63.0)  (double constants:
+//                   the float product (q - p) * v is promoted, the sum rounded once)
+int parse_payload(Reader& r, int kind, int rows, int cols, float* out, int cm_kaldi = 0) {
   const size_t n = (size_t)rows * cols;
   if (kind == 0) {
     if (!r.take(out, n * 4)) return kfail(VOX_EIO, "truncated FM payload");
@@ -132,15 +141,31 @@ int parse_payload(Reader& r, int kind, int rows, int cols, float* out) {
   for (int col = 0; col < cols; ++col) {
     float p[4];
     for (int k = 0; k < 4; ++k) {
-      // kaldi_io: uint16 * float32(range) * float32(1/65535) + float32(min), float32 ops
-      float v = (float)ch[(size_t)col * 4 + k] * range;
-      v = v * c;
-      p[k] = v + mn;
+      const float u = (float)ch[(size_t)col * 4 + k];
+      if (cm_kaldi) {
+        p[k] = mn + (range * c) * u;
+      } else {
+        // kaldi_io: uint16 * float32(range) * float32(1/65535) + float32(min), float32 ops
+        float v = u * range;
+        v = v * c;
+        p[k] = v + mn;
+      }
+    }
+    const uint8_t* d = &data[(size_t)col * rows];  // column-major
+    if (cm_kaldi) {
+      for (int row = 0; row < rows; ++row) {
+        const unsigned v = d[row];
+        double x;
+        if (v <= 64) x = (double)p[0] + (double)((p[1] - p[0]) * (float)v) * (1 / 64.0);
+        else if (v <= 192) x = (double)p[1] + (double)((p[2] - p[1]) * (float)(v - 64)) * (1 / 128.0);
+        else x = (double)p[2] + (double)((p[3] - p[2]) * (float)(v - 192)) * (1 / 63.0);
+        out[(size_t)row * cols + col] = (float)x;
+      }
+      continue;
     }
     const float s0 = (p[1] - p[0]) / 64.0f;
     const float s1 = (p[2] - p[1]) / 128.0f;
     const float s2 = (p[3] - p[2]) / 63.0f;
-    const uint8_t* d = &data[(size_t)col * rows];  // column-major
     for (int row = 0; row < rows; ++row) {
       const unsigned v = d[row];
       float x;
@@ -204,18 +229,28 @@ extern "C" int vox_parse_mat_shape(const uint8_t* buf, size_t nbytes, int* rows,
   return parse_header(r, rows, cols, &kind);
 }
 
-extern "C" int vox_parse_mat(const uint8_t* buf, size_t nbytes, float* out, int rows, int cols,
-                             size_t* consumed) {
+static int parse_mat(const uint8_t* buf, size_t nbytes, float* out, int rows, int cols,
+                     size_t* consumed, int cm_kaldi) {
   if (!buf || (!out && rows * cols > 0)) return kfail(VOX_EINVAL, "null argument");
   Reader r{buf, nbytes};
   int nr, nc, kind;
   int rc = parse_header(r, &nr, &nc, &kind);
   if (rc) return rc;
   if (nr != rows || nc != cols) return kfail(VOX_EINVAL, "matrix shape mismatch");
-  rc = parse_payload(r, kind, nr, nc, out);
+  rc = parse_payload(r, kind, nr, nc, out, cm_kaldi);
   if (rc) return rc;
   if (consumed) *consumed = r.i;
   return VOX_OK;
+}
+
+extern "C" int vox_parse_mat(const uint8_t* buf, size_t nbytes, float* out, int rows, int cols,
+                             size_t* consumed) {
+  return parse_mat(buf, nbytes, out, rows, cols, consumed, 0);
+}
+
+extern "C" int vox_parse_mat_kaldi(const uint8_t* buf, size_t nbytes, float* out, int rows,
+                                   int cols, size_t* consumed) {
+  return parse_mat(buf, nbytes, out, rows, cols, consumed, 1);
 }
 
 extern "C" int vox_mat_shape(const char* path, int64_t offset, int* rows, int* cols) {
@@ -226,12 +261,22 @@ extern "C" int vox_mat_shape(const char* path, int64_t offset, int* rows, int* c
   return vox_parse_mat_shape(buf.data(), buf.size(), rows, cols);
 }
 
-extern "C" int vox_read_mat(const char* path, int64_t offset, float* out, int rows, int cols) {
+static int read_mat(const char* path, int64_t offset, float* out, int rows, int cols,
+                    int cm_kaldi) {
   if (!path) return kfail(VOX_EINVAL, "null argument");
   std::vector<uint8_t> buf;
   int rc = read_file_at(path, offset, buf);
   if (rc) return rc;
-  return vox_parse_mat(buf.data(), buf.size(), out, rows, cols, nullptr);
+  return parse_mat(buf.data(), buf.size(), out, rows, cols, nullptr, cm_kaldi);
+}
+
+extern "C" int vox_read_mat(const char* path, int64_t offset, float* out, int rows, int cols) {
+  return read_mat(path, offset, out, rows, cols, 0);
+}
+
+extern "C" int vox_read_mat_kaldi(const char* path, int64_t offset, float* out, int rows,
+                                  int cols) {
+  return read_mat(path, offset, out, rows, cols, 1);
 }
 
 extern "C" int64_t vox_format_vec_flt(const char* key, const float* v, int dim, uint8_t* buf,

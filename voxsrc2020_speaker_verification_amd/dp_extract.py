@@ -50,6 +50,17 @@ def gather_embeddings(keys, emb, group=None, device=None):
     return all_keys, (np.concatenate(mats, 0) if mats else np.zeros((0, dim), np.float32))
 
 
+def rank_failures(failed, device=None, group=None):
+    """All-gather one failure flag per rank; returns the failed rank ids."""
+    import torch
+    import torch.distributed as dist
+    dev = device if device is not None else torch.device("cpu")
+    flag = torch.tensor([1 if failed else 0], dtype=torch.int64, device=dev)
+    flags = [torch.zeros_like(flag) for _ in range(dist.get_world_size(group))]
+    dist.all_gather(flags, flag, group=group)
+    return [r for r, f in enumerate(flags) if int(f.item())]
+
+
 def run(rank, world, scp_items, embed_fn, dim, wspec, shard_file=None, batch=64,
         device=None, write_per_rank=True, cohort_spk2utt=None):
     """The per-rank body (also used by the gloo tests with a fake embedder).
@@ -57,11 +68,24 @@ def run(rank, world, scp_items, embed_fn, dim, wspec, shard_file=None, batch=64,
     decodes its own shard: `scp_items` is a callable(rank, world) -> list of
     (key, [T,F] features)."""
     from .extract import embed_utterances, write_vectors
-    feats = scp_items(rank, world)
-    emb = embed_utterances(feats, embed_fn, dim, batch) if feats else np.zeros((0, dim), np.float32)
-    keys = [k for k, _ in feats]
-    if write_per_rank and wspec:
-        write_vectors(f"{wspec}.{rank + 1}", keys, emb)   # xvector.<i>.ark as the reference
+    err = None
+    try:
+        feats = scp_items(rank, world)
+        emb = (embed_utterances(feats, embed_fn, dim, batch) if feats
+               else np.zeros((0, dim), np.float32))
+        keys = [k for k, _ in feats]
+        if write_per_rank and wspec:
+            write_vectors(f"{wspec}.{rank + 1}", keys, emb)   # xvector.<i>.ark as the reference
+    except Exception as e:   # e.g. ZeroDivisionError for a < 25-frame utterance
+        err = e
+    # every rank learns whether any shard failed BEFORE the gathers, so no rank
+    # is left blocked in a collective (the reference's per-shard processes fail
+    # independently, eval_inference_model.sh:29-36)
+    failed = rank_failures(err is not None, device)
+    if failed:
+        if err is not None:
+            raise err
+        raise RuntimeError(f"extraction failed on rank(s) {failed}; rank {rank} aborts too")
     all_keys, all_emb = gather_embeddings(keys, emb, device=device)
     if rank == 0 and wspec:
         write_vectors(wspec, all_keys, all_emb)           # == cat xvector.{1..N}.ark
@@ -109,7 +133,7 @@ def main(argv=None):
         out = []
         for key, rx in lines:
             path, off, rng = parse_rxfile(rx)
-            m = read_mat(path, off)
+            m = read_mat(path, off, cm="kaldi")   # Kaldi decodes CM in the reference pipe
             if rng is not None:
                 m = np.ascontiguousarray(m[rng])
             out.append((key, sliding_cmn(m)))

@@ -57,22 +57,37 @@ def parse_rxfile(rx):
     return rx, 0, rng
 
 
-def read_mat(path, offset=0):
-    """Binary Kaldi matrix (FM / DM / CM) at `offset` -> float32 [rows, cols]."""
+CM_DECODE = ("kaldi_io", "kaldi")
+
+
+def _cm_fn(cm, name):
+    if cm not in CM_DECODE:
+        raise ValueError(f"cm must be one of {CM_DECODE}")
+    return getattr(lib(), name + ("_kaldi" if cm == "kaldi" else ""))
+
+
+def read_mat(path, offset=0, cm="kaldi_io"):
+    """Binary Kaldi matrix (FM / DM / CM) at `offset` -> float32 [rows, cols].
+    cm="kaldi_io": compressed payloads decoded in kaldi_io._read_compressed_mat's
+    arithmetic (the reference's Python reader); cm="kaldi": in Kaldi C++'s
+    CompressedMatrix arithmetic (what the reference's apply-cmvn-sliding pipe
+    decodes, tf_extract.py:63)."""
     r, c = C.c_int(), C.c_int()
     check(lib().vox_mat_shape(os.fsencode(path), int(offset), C.byref(r), C.byref(c)))
     out = np.empty((r.value, c.value), np.float32)
-    check(lib().vox_read_mat(os.fsencode(path), int(offset), fptr(out), r.value, c.value))
+    check(_cm_fn(cm, "vox_read_mat")(os.fsencode(path), int(offset), fptr(out), r.value,
+                                     c.value))
     return out
 
 
-def parse_mat(buf):
+def parse_mat(buf, cm="kaldi_io"):
     """Binary matrix from bytes starting at '\\0B' -> (float32 array, bytes used)."""
     r, c = C.c_int(), C.c_int()
     check(lib().vox_parse_mat_shape(buf, len(buf), C.byref(r), C.byref(c)))
     out = np.empty((r.value, c.value), np.float32)
     used = C.c_size_t()
-    check(lib().vox_parse_mat(buf, len(buf), fptr(out), r.value, c.value, C.byref(used)))
+    check(_cm_fn(cm, "vox_parse_mat")(buf, len(buf), fptr(out), r.value, c.value,
+                                      C.byref(used)))
     return out, used.value
 
 
@@ -81,7 +96,7 @@ def _read_key(buf, pos):
     return buf[pos:end].decode("utf-8").strip(), end + 1
 
 
-def read_mat_ark(path):
+def read_mat_ark(path, cm="kaldi_io"):
     """Generator of (key, matrix) over an ark of binary matrices (kaldi_io.read_mat_ark)."""
     with open(path, "rb") as f:
         buf = f.read()
@@ -90,7 +105,7 @@ def read_mat_ark(path):
         key, pos = _read_key(buf, pos)
         if not key:
             break
-        mat, used = parse_mat(buf[pos:])
+        mat, used = parse_mat(buf[pos:], cm)
         pos += used
         yield key, mat
 
@@ -104,11 +119,12 @@ def sliding_cmn(x, cmn_window=CMN_WINDOW, center=True):
     return out
 
 
-def iter_features(scp_path, cmn=True):
-    """(key, float32 [T, F]) in scp order: the tf_extract rspec pipeline."""
+def iter_features(scp_path, cmn=True, cm="kaldi"):
+    """(key, float32 [T, F]) in scp order: the tf_extract rspec pipeline
+    (Kaldi decodes compressed arks there, hence cm="kaldi")."""
     for key, rx in read_scp(scp_path):
         path, off, rng = parse_rxfile(rx)
-        mat = read_mat(path, off)
+        mat = read_mat(path, off, cm)
         if rng is not None:
             mat = np.ascontiguousarray(mat[rng])
         yield key, (sliding_cmn(mat) if cmn else mat)

@@ -94,14 +94,16 @@ def cohort_mean_std_gpu(trial_xvectors, cohort, topk=400, device=0):
     trial = np.ascontiguousarray(np.array(list(trial_xvectors.values())), dtype=np.float32)
     cmat = np.ascontiguousarray(np.array(list(cohort.values())), dtype=np.float32)
     dev = torch.device("cuda", device)
-    td, cd = torch.from_numpy(trial).to(dev), torch.from_numpy(cmat).to(dev)
-    md = torch.empty(len(utt), dtype=torch.float32, device=dev)
-    sd = torch.empty_like(md)
-    stream = torch.cuda.current_stream(dev).cuda_stream
-    check(lib().vox_asnorm_stats(C.c_void_p(td.data_ptr()), trial.shape[0],
-                                 C.c_void_p(cd.data_ptr()), cmat.shape[0], trial.shape[1],
-                                 int(topk), C.c_void_p(md.data_ptr()), C.c_void_p(sd.data_ptr()),
-                                 C.c_void_p(stream)))
+    # the library also selects the operands' device itself (hipPointerGetAttributes)
+    with torch.cuda.device(dev):
+        td, cd = torch.from_numpy(trial).to(dev), torch.from_numpy(cmat).to(dev)
+        md = torch.empty(len(utt), dtype=torch.float32, device=dev)
+        sd = torch.empty_like(md)
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        check(lib().vox_asnorm_stats(C.c_void_p(td.data_ptr()), trial.shape[0],
+                                     C.c_void_p(cd.data_ptr()), cmat.shape[0], trial.shape[1],
+                                     int(topk), C.c_void_p(md.data_ptr()),
+                                     C.c_void_p(sd.data_ptr()), C.c_void_p(stream)))
     m, s = md.cpu().numpy(), sd.cpu().numpy()
     return ({u: m[i] for i, u in enumerate(utt)}, {u: s[i] for i, u in enumerate(utt)})
 
