@@ -32,6 +32,8 @@ PEAK_HBM_GBS = 8000.0       # HBM3E spec
 
 def _kernel_name(tag, dt):
     kind = tag & 15
+    if tag & (1 << 30):
+        return "gemm1x1_wide"
     if tag & (1 << 29):
         return "conv3x3_pipe"
     if tag & (1 << 28):
@@ -215,6 +217,12 @@ def main():
     dom_name, dom = max(conv.items(), key=lambda kv: kv[1]["ms"])
     peak = PEAK_F32_TFLOPS if "float" in dom_name else PEAK_BF16_TFLOPS
     ach = (dom["flops"] / dom["n"]) / (dom["ms"] / dom["n"] * 1e-3) / 1e12
+    # which roof bounds the dominant kernel: the larger of its FLOP time at the
+    # dense MFMA peak and its algorithmic-byte time at the HBM peak (the 1x1
+    # GEMMs at B=256 are 70-440 FLOP/B against a machine balance of ~310)
+    t_mfma = dom["flops"] / (peak * 1e12)
+    t_hbm = dom["bytes"] / (PEAK_HBM_GBS * 1e9)
+    ach_gbs = (dom["bytes"] / dom["n"]) / (dom["ms"] / dom["n"] * 1e-3) / 1e9
     fwd_ms = float(np.sum(prof["ms"]))
     conv_fl = sum(v["flops"] for v in conv.values())
     conv_ms = sum(v["ms"] for v in conv.values())
@@ -224,13 +232,24 @@ def main():
     pmc_ok = ((args.model, F, T, B, args.precision)
               == ("res2net50_w24_s4_c32", 80, 200, 256, "bf16"))
     traffic = pmc_traffic if pmc_ok else (lambda k: None)
-    roof = {"bound": "mfma", "kernel": dom_name, "launches_per_step": dom["n"],
-            "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
-            "frac": round(ach / peak, 4), "traffic": traffic(dom_name),
-            "traffic_unit": "HBM bytes per launch (rocprofv3 PMC, profiles/pmc_summary.json)",
-            "algorithmic_bytes_per_launch": dom["bytes"] / dom["n"],
-            "avg_launch_us": round(dom["ms"] / dom["n"] * 1e3, 2),
-            "flop_per_launch": dom["flops"] / dom["n"]}
+    if t_hbm >= t_mfma:
+        roof = {"bound": "hbm", "kernel": dom_name, "launches_per_step": dom["n"],
+                "achieved": round(ach_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": round(ach_gbs / PEAK_HBM_GBS, 4)}
+    else:
+        roof = {"bound": "mfma", "kernel": dom_name, "launches_per_step": dom["n"],
+                "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
+                "frac": round(ach / peak, 4)}
+    roof.update({
+        "traffic": traffic(dom_name),
+        "traffic_unit": "HBM bytes per launch (rocprofv3 PMC, profiles/pmc_summary.json)",
+        "algorithmic_bytes_per_launch": dom["bytes"] / dom["n"],
+        "avg_launch_us": round(dom["ms"] / dom["n"] * 1e3, 2),
+        "flop_per_launch": dom["flops"] / dom["n"],
+        "mfma_tflops": round(ach, 2), "mfma_frac": round(ach / peak, 4),
+        "hbm_gbs": round(ach_gbs, 1), "hbm_frac": round(ach_gbs / PEAK_HBM_GBS, 4),
+        # fraction of the kernel's own roofline time max(FLOP/peak, bytes/BW)
+        "roofline_frac": round(max(t_mfma, t_hbm) / (dom["ms"] * 1e-3), 4)})
     extra = {
         "conv_stack": {"achieved_tflops": round(conv_fl / (conv_ms * 1e-3) / 1e12, 2),
                        "frac": round(conv_fl / (conv_ms * 1e-3) / 1e12 / peak, 4),

@@ -233,6 +233,7 @@ def test_gemm_pipe_bitwise_many_tiles(weights, N, T, monkeypatch):
     from voxsrc2020_speaker_verification_amd import synth
     spec, t, blob = weights("res2net50_w24_s4_c32", 80)
     x = synth.make_features(N, T, 80, seed=9)
+    monkeypatch.setenv("VOXEMB_NO_GEMM_WIDE", "1")
     with _extractor(blob, "bf16") as ex:
         pipe = ex.run(x)
         assert any(l.startswith("gemmpipe") for l in ex.describe(torch.from_numpy(x).cuda()))
@@ -241,6 +242,30 @@ def test_gemm_pipe_bitwise_many_tiles(weights, N, T, monkeypatch):
         ref = ex.run(x)
         assert not any(l.startswith("gemmpipe") for l in ex.describe(torch.from_numpy(x).cuda()))
     assert np.array_equal(pipe, ref)
+
+
+@pytest.mark.parametrize("name,F,T,N", [("res2net50_w24_s4_c32", 80, 200, 16),
+                                        ("res2net50_w24_s4_c32", 80, 123, 7),
+                                        ("res2net50_w24_s4_c64", 40, 75, 3),
+                                        ("res2net101_w24_s4_c32_att", 80, 64, 3),
+                                        ("tdnn", 80, 200, 40)])
+def test_gemm_wide_bitwise_pipe(weights, name, F, T, N, monkeypatch):
+    """The wide-tile GEMM (256 x 256 / 256 x 192 tiles, 4-slot BK=32 ring,
+    residual streamed as extra DMA phases, ragged last pixel tile, dual
+    destination of the 1x1a) gives the same bits as gemm1x1_pipe."""
+    import torch
+    from voxsrc2020_speaker_verification_amd import synth
+    spec, t, blob = weights(name, F)
+    x = synth.make_features(N, T, F, seed=29)
+    with _extractor(blob, "bf16") as ex:
+        got = ex.run(x)
+        desc = ex.describe(torch.from_numpy(x).cuda())
+        assert any(l.startswith("gemmwide") for l in desc), desc
+    monkeypatch.setenv("VOXEMB_NO_GEMM_WIDE", "1")
+    with _extractor(blob, "bf16") as ex:
+        ref = ex.run(x)
+        assert not any(l.startswith("gemmwide") for l in ex.describe(torch.from_numpy(x).cuda()))
+    assert np.array_equal(got, ref)
 
 
 @pytest.mark.parametrize("name,F,T,N", [("res2net50_w24_s4_c32", 80, 200, 4),
@@ -299,3 +324,21 @@ def test_bneck_segments_bitwise(weights, monkeypatch):
         assert any(l.startswith("bneck") for l in ex.describe(torch.from_numpy(x).cuda()))
         for i in range(4):
             assert np.array_equal(ex.run(x[i:i + 1])[0], full[i])
+
+
+@pytest.mark.parametrize("name,F,T,N", [("res2net50_w24_s4_c32", 80, 200, 5), ("tdnn", 40, 320, 3),
+                                        ("dpn68", 80, 64, 2)])
+def test_graph_replay_equals_eager(weights, name, F, T, N, monkeypatch):
+    """The plan replayed as one captured hipGraph gives the same bits as eager
+    launches, across repeated calls, new inputs and a new batch shape."""
+    from voxsrc2020_speaker_verification_amd import synth
+    spec, t, blob = weights(name, F)
+    xs = [synth.make_features(N, T, F, seed=s) for s in (1, 2)] + \
+         [synth.make_features(N + 1, T, F, seed=3)]
+    with _extractor(blob, "bf16") as ex:
+        got = [ex.run(x) for x in xs] + [ex.run(xs[0])]
+    monkeypatch.setenv("VOXEMB_NO_GRAPH", "1")
+    with _extractor(blob, "bf16") as ex:
+        ref = [ex.run(x) for x in xs] + [ex.run(xs[0])]
+    for a, b in zip(got, ref):
+        assert np.array_equal(a, b)

@@ -17,6 +17,7 @@ SOURCES = [
     ("bneck.hip", ["-O3"]),
     ("asnorm.hip", ["-O3"]),
     ("gemm.hip", ["-O3"]),
+    ("gemm_wide.hip", ["-O3"]),
     ("gconv.hip", ["-O3"]),
     ("conv3.hip", ["-O3"]),
     ("api.cpp", ["-O2"]),

@@ -217,6 +217,10 @@ struct vox_model {
   const float* plan_x = nullptr;
   float* plan_out = nullptr;
   std::vector<Op> plan;
+  // the plan's launches captured once into a hipGraph and replayed per call
+  // (VOXEMB_NO_GRAPH=1: eager launches); rebuilt with the plan
+  bool use_graph = true;
+  hipGraphExec_t graph_exec = nullptr;
   DevBuf stage_in, stage_out;  // host-API staging
   float eps4 = 1.001e-5f, eps2 = 1e-5f;  // BN epsilons (blob header may override)
   bool no_win = false;         // VOXEMB_NO_WIN=1: disable conv_win (A/B testing)
@@ -224,6 +228,7 @@ struct vox_model {
   bool no_rr = false;          // VOXEMB_NO_RR=1: disable conv1x1_rr
   bool no_gemm = false;        // VOXEMB_NO_GEMM=1: disable gemm1x1_lds
   bool no_gemm_pipe = false;   // VOXEMB_NO_GEMM_PIPE=1: gemm1x1_lds instead of gemm1x1_pipe
+  bool no_gemm_wide = false;   // VOXEMB_NO_GEMM_WIDE=1: gemm1x1_pipe instead of gemm1x1_wide
   bool no_gconv = false;       // VOXEMB_NO_GCONV=1: grouped 3x3 on the generic implicit GEMM
   bool no_conv3 = false;
   bool no_gemm_pro = false;    // VOXEMB_NO_GEMM_PRO=1: prologue 1x1 convs off the pipelined GEMM       // VOXEMB_NO_CONV3=1: Res2Net w>=96 3x3 branches on conv_win/igemm
@@ -594,6 +599,9 @@ static void emit_conv(Builder& B, const ConvW& cw, Act x, const void* x2, int ld
       p.coutp = cout128;
       // persistent LDS-DMA pipelined GEMM (gemm.hip) where its tiling applies
       if (!B.m->no_gemm_pipe && gemm_pipe_ok(p)) op.type = 18;
+      // wide-tile variant (gemm_wide.hip): 256 x 256 / 256 x 192 tiles, residual
+      // streamed through the DMA ring
+      if (!B.m->no_gemm_wide && gemm_wide_bn(p)) op.type = 21;
     }
   }
   // bf16 1x1 with a BN+ReLU input prologue (DPN bn_relu_conv): the pipelined
@@ -1259,6 +1267,10 @@ static int build_plan(vox_model* m, const float* x, int n, int t, float* out) {
     if (m->family == "dpn") return build_dpn(B, x, n, t, out);
     return fail(VOX_EINVAL, "unknown family");
   };
+  if (m->graph_exec) {
+    (void)hipGraphExecDestroy(m->graph_exec);
+    m->graph_exec = nullptr;
+  }
   int rc = run(true);
   if (rc) return rc;
   for (int s = 0; s < S_NSLOTS; ++s) HIPCHK(m->slots[s].ensure(m->slot_need[s]));
@@ -1280,6 +1292,7 @@ static hipError_t run_op(vox_model* m, const Op& op, hipStream_t s) {
     case 18: return launch_gemm_pipe(op.cp, m->num_cu, m->gemm_var, s);
     case 19: return launch_gconv(op.gq, s);
     case 20: return launch_conv3_pipe(op.cp, m->num_cu, s);
+    case 21: return launch_gemm_wide(op.cp, m->num_cu, s);
     case 10: return launch_split_chain(op.ch, op.cl.wco, op.cl.wpx, s);
     case 12: return launch_bneck(op.bq, op.cin, op.C, op.cl.wco, op.S, s);
     case 13: return launch_chain_rows(op.ch, s);
@@ -1355,6 +1368,8 @@ extern "C" int vox_load_blob(const void* blob, size_t nbytes, int device, int pr
   if (const char* e = std::getenv("VOXEMB_RR_WPX")) m->rr_wpx = std::atoi(e);
   if (const char* e = std::getenv("VOXEMB_NO_GEMM")) m->no_gemm = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_NO_GEMM_PIPE")) m->no_gemm_pipe = std::atoi(e) != 0;
+  if (const char* e = std::getenv("VOXEMB_NO_GEMM_WIDE")) m->no_gemm_wide = std::atoi(e) != 0;
+  if (const char* e = std::getenv("VOXEMB_NO_GRAPH")) m->use_graph = std::atoi(e) == 0;
   if (const char* e = std::getenv("VOXEMB_NO_GCONV")) m->no_gconv = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_NO_CONV3")) m->no_conv3 = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_NO_GEMM_PRO")) m->no_gemm_pro = std::atoi(e) != 0;
@@ -1392,6 +1407,8 @@ extern "C" void vox_free(vox_model* m) {
     (void)hipStreamSynchronize(m->stream);
     (void)hipStreamDestroy(m->stream);
   }
+  (void)hipDeviceSynchronize();   // replays launched on callers' streams
+  if (m->graph_exec) (void)hipGraphExecDestroy(m->graph_exec);
   delete m;
 }
 
@@ -1410,6 +1427,29 @@ extern "C" int vox_embed_device(vox_model* m, const float* d_x, int n, int t, in
   HIPCHK(hipSetDevice(m->device));
   if ((rc = ensure_plan(m, d_x, n, t, d_out))) return rc;
   hipStream_t s = stream ? (hipStream_t)stream : m->stream;
+  if (m->use_graph && !m->graph_exec) {
+    // capture on the handle's own stream (the caller's may be the legacy null
+    // stream, which cannot be captured); the exec then launches on any stream
+    hipGraph_t g = nullptr;
+    hipError_t e = hipStreamBeginCapture(m->stream, hipStreamCaptureModeThreadLocal);
+    if (e == hipSuccess) {
+      for (const Op& op : m->plan)
+        if ((e = run_op(m, op, m->stream)) != hipSuccess) break;
+      hipError_t e2 = hipStreamEndCapture(m->stream, &g);
+      if (e == hipSuccess) e = e2;
+    }
+    if (e == hipSuccess) e = hipGraphInstantiate(&m->graph_exec, g, nullptr, nullptr, 0);
+    if (g) (void)hipGraphDestroy(g);
+    if (e != hipSuccess) {   // launch eagerly from now on (same kernels)
+      (void)hipGetLastError();
+      m->graph_exec = nullptr;
+      m->use_graph = false;
+    }
+  }
+  if (m->use_graph && m->graph_exec) {
+    HIPCHK(hipGraphLaunch(m->graph_exec, s));
+    return VOX_OK;
+  }
   for (const Op& op : m->plan) HIPCHK(run_op(m, op, s));
   return VOX_OK;
 }
@@ -1508,6 +1548,8 @@ extern "C" int vox_profile(vox_model* m, const float* d_x, int n, int t, int f, 
         tag |= (1 << 28);
       else if (o.type == 20)
         tag |= (1 << 29);
+      else if (o.type == 21)
+        tag |= (1 << 30);
       else if (o.type == 8)
         tag |= (o.cl.wco << 4) | (o.cl.wpx << 8) | (((o.cp.cinp + 31) / 32) << 16) | (1 << 20);
       else if (o.type == 0 || o.type == 5)
@@ -1530,12 +1572,13 @@ extern "C" int vox_plan_describe(vox_model* m, const float* d_x, int n, int t, i
   std::string out;
   static const char* tn[] = {"igemm", "reduce", "pool", "avgpool", "convert", "igemm32", "bnrelu",
                              "win", "rr", "gemm", "chain", "stem", "bneck", "chainrows", "splits2",
-                             "cvt16", "atttanh", "attpool", "gemmpipe", "gconv", "conv3pipe"};
+                             "cvt16", "atttanh", "attpool", "gemmpipe", "gconv", "conv3pipe",
+                             "gemmwide"};
   for (const Op& o : m->plan) {
     char line[256];
     const ConvParams& p = o.cp;
     if (o.type == 0 || o.type == 5 || o.type == 7 || o.type == 8 || o.type == 9 || o.type == 18 ||
-        o.type == 20)
+        o.type == 20 || o.type == 21)
       std::snprintf(line, sizeof(line),
                     "%s wco=%d wpx=%d s=%d N=%d H=%d W=%d Cin=%d Ho=%d Wo=%d Cout=%d k=%dx%d st=%d "
                     "g=%d flags=%d x2=%d pro=%d flops=%.4g bytes=%.4g\n",

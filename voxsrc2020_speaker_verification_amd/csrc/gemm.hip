@@ -90,7 +90,9 @@ template <int N> __device__ __forceinline__ void wait_vm() {
 // start, one extra barrier per step); channels k >= Cin are zero, as in the
 // generic conv.  K may end on a half step (kp % 64 = 32): the tail DMA reads
 // a zero line and the all-zero MFMA half step is skipped.
-template <int SWZ, bool PRO>
+// DBG (diagnostics only, VOXEMB_GEMM_VAR=2/3): 1 = no MFMA / fragment reads,
+// 2 = no operand DMA (MFMAs on whatever the ring holds); results are garbage
+template <int SWZ, bool PRO, int DBG = 0>
 __global__ __launch_bounds__(GP_NT) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void gemm1x1_pipe(ConvParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -167,11 +169,13 @@ void gemm1x1_pipe(ConvParams p) {
     const uint32_t base = lds_wave + (uint32_t)s_slot * GP_SLOT;
     const int ko = l_k * 64;
     const bool kin = !PRO || ko + cch * 8 < p.kp;
+    if (DBG == 2) goto advance;
 #pragma unroll
     for (int i = 0; i < GP_NA; ++i) glds16(kin ? pa[i] + ko : gzero, base + i * 8192u);
 #pragma unroll
     for (int i = 0; i < GP_NB; ++i) glds16(kin ? pb[i] + ko : gzero, base + (GP_NA + i) * 8192u);
     // advance; past the last tile the final step is re-read (never consumed)
+  advance:
     if (l_k + 1 < KT) {
       ++l_k;
     } else if (l_tile + 1 < ntiles) {
@@ -307,6 +311,7 @@ void gemm1x1_pipe(ConvParams p) {
     const char* L = smem + sb;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
+      if (DBG == 1) break;
       if (PRO && ks == 1 && last && (p.kp & 63)) break;   // zero half step past kp
       const int cs = ((ks * 4 + g) ^ swa) << 4;
       bf16x8 a[4], b[4];
@@ -425,6 +430,10 @@ hipError_t launch_gemm_pipe(const ConvParams& p, int num_cu, int variant, hipStr
                        GP_NST * GP_SLOT + 8 * p.kp, s, p);
   else if (variant == 1)
     hipLaunchKernelGGL((gemm1x1_pipe<0, false>), dim3(G), dim3(GP_NT), GP_NST * GP_SLOT, s, p);
+  else if (variant == 2)
+    hipLaunchKernelGGL((gemm1x1_pipe<1, false, 1>), dim3(G), dim3(GP_NT), GP_NST * GP_SLOT, s, p);
+  else if (variant == 3)
+    hipLaunchKernelGGL((gemm1x1_pipe<1, false, 2>), dim3(G), dim3(GP_NT), GP_NST * GP_SLOT, s, p);
   else
     hipLaunchKernelGGL((gemm1x1_pipe<1, false>), dim3(G), dim3(GP_NT), GP_NST * GP_SLOT, s, p);
   return hipGetLastError();

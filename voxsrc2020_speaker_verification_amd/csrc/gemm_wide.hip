@@ -1,0 +1,364 @@
+// Wide-tile persistent LDS-DMA GEMM for the bf16 1x1 convolutions of the
+// Res2Net bottlenecks (conv1x1a / conv1x1c / projection shortcut,
+// res2net_model.py:90-127 via tf_extract.py) and the TDNN 1x1 layers.
+//
+// Why: gemm1x1_pipe (gemm.hip) is bound by what a CU can pull through its
+// memory pipe, not by MFMA (profiles: removing its MFMAs saves ~4 %, removing
+// its operand DMA ~25 %).  Its 256-pixel x 128-cout tile re-reads every pixel
+// row once per 128 output channels.  Here a tile is 256 pixels x BN couts
+// (BN = 256, or 192 for the 192/384/768-channel 1x1a), so per output element
+// the operand bytes a CU moves drop by a third (L3 1x1c: 6.5 -> 4.3 KB per
+// pixel including the epilogue), and:
+//   * BK = 32: a ring slot is (BN + 256) rows x 64 B (<= 32 KB), 4 slots,
+//     three K-steps in flight (96 KB per CU) while one is computed;
+//   * 8 waves as 2 (cout halves) x 4 (64-pixel quarters): a wave owns
+//     BN/2 couts x 64 pixels = (BN/32) x 4 MFMA 16x16x32 accumulators;
+//   * the residual tile of the 1x1c (res2net_model.py:100) is streamed by the
+//     same DMA ring as four extra "phase" steps after the K-steps (64 pixels x
+//     256 couts = 32 KB each): no residual registers, its latency covered like
+//     an operand's, and the epilogue of 16-pixel column j runs in phase j;
+//   * BN parameters of all output channels sit in LDS for the whole kernel.
+// LDS operand rows are 64 B; 16-B chunk c of row r is stored at position
+// c ^ f((r >> 2) & 3), f(a) = (4 - a) & 3, which makes the ds_read_b128
+// fragment reads conflict-free under gfx950's 4 x 16-lane read groups (DMA
+// writes are lane-linear, so the swizzle is applied to each lane's SOURCE
+// chunk).  Residual rows are 512 B, chunk c at c ^ (r & 15).
+// Accumulation order per output = K chunks of 32 in increasing order, and the
+// epilogue is the same sequence of roundings: bitwise identical to
+// gemm1x1_pipe / gemm1x1_lds.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <type_traits>
+
+#include "device_common.h"
+#include "kernels.h"
+
+namespace vox {
+
+namespace {
+constexpr int GW_BM = 256;      // pixels per tile
+constexpr int GW_NT = 512;      // 8 waves
+constexpr int GW_NST = 4;       // ring slots
+constexpr int GW_SLOT = 32768;  // bytes per ring slot
+constexpr int GW_NR = 4;        // residual phases per tile
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void gw_glds16(const void* src, uint32_t lds) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(lds)
+      : "memory");
+}
+
+// the trailing s_nop keeps the next instruction from overwriting the data
+// registers before the store has read them
+__device__ __forceinline__ void gw_st16(void* dst, u32x4 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" : : "v"(dst), "v"(v) : "memory");
+}
+
+#define GW_W(n) \
+  case n: asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory"); break;
+// s_waitcnt with a wave-uniform count (a scalar branch to the immediate form)
+__device__ __forceinline__ void gw_wait_vm(int n) {
+  switch (n) {
+    GW_W(0) GW_W(1) GW_W(2) GW_W(3) GW_W(4) GW_W(5) GW_W(6) GW_W(7) GW_W(8) GW_W(9)
+    GW_W(10) GW_W(11) GW_W(12) GW_W(13) GW_W(14) GW_W(15) GW_W(16) GW_W(17) GW_W(18)
+    GW_W(19) GW_W(20) GW_W(21) GW_W(22) GW_W(23) GW_W(24) GW_W(25) GW_W(26) GW_W(27)
+    GW_W(28) GW_W(29) GW_W(30) GW_W(31) GW_W(32)
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+  __builtin_amdgcn_sched_barrier(0);
+}
+#undef GW_W
+
+__device__ __forceinline__ int gw_swz(int r) { return (4 - ((r >> 2) & 3)) & 3; }
+}  // namespace
+
+__device__ uint4 g_gw_sink[64];   // destination of masked lanes' stores
+
+#pragma clang fp contract(off)
+template <int BN, bool RES>
+__global__ __launch_bounds__(GW_NT) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void gemm1x1_wide(ConvParams p) {
+  constexpr int NI = BN / 32;                // 16-cout MFMA blocks per wave (BN/2 couts)
+  constexpr int NQ = NI / 2;                 // 32-cout groups per wave
+  constexpr int GRP = (BN + GW_BM) / 16;     // 1-KB DMA groups per operand step
+  constexpr int NLMAX = (GRP + 7) / 8;
+  constexpr int NR = RES ? GW_NR : 0;
+  static_assert(!RES || GRP == 32, "residual phases need 4 DMA groups per wave");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int col = lane & 15, g = lane >> 4;
+  const int NLw = (wave + 8 * (NLMAX - 1) < GRP) ? NLMAX : NLMAX - 1;   // wave-uniform
+  const int M = p.N * p.Ho * p.Wo;
+  const int HoWo = p.Ho * p.Wo;
+  const int KT = p.kp / 32;
+  const int SPT = KT + NR;                   // ring steps per tile
+  const int cblocks = p.coutp / BN;
+  const int T = ((M + GW_BM - 1) / GW_BM) * cblocks;
+  // tiles of this workgroup: XCD x (blocks x, x+8, ...) owns the contiguous
+  // range [x*T/8, (x+1)*T/8) and its nb workgroups take every nb-th tile, so at
+  // any moment one XCD works on nb consecutive tiles (the cout blocks of a
+  // pixel block share its L2 lines)
+  int t_first, t_step, ntiles;
+  {
+    const int G = gridDim.x;
+    if ((G & 7) == 0) {
+      const int x = blockIdx.x & 7, bi = blockIdx.x >> 3, nb = G >> 3;
+      const int b0 = (int)((long)x * T / 8), b1 = (int)((long)(x + 1) * T / 8);
+      t_first = b0 + bi;
+      t_step = nb;
+      ntiles = t_first < b1 ? (b1 - t_first + nb - 1) / nb : 0;
+    } else {
+      t_first = blockIdx.x;
+      t_step = G;
+      ntiles = t_first < T ? (T - t_first + G - 1) / G : 0;
+    }
+  }
+  if (ntiles == 0) return;
+  const int S = ntiles * SPT;
+
+  const bf16_t* __restrict__ X = reinterpret_cast<const bf16_t*>(p.x);
+  const bf16_t* __restrict__ Wt = reinterpret_cast<const bf16_t*>(p.w);
+  const bf16_t* __restrict__ R = reinterpret_cast<const bf16_t*>(p.res);
+  bf16_t* __restrict__ Y = reinterpret_cast<bf16_t*>(p.y);
+  bf16_t* __restrict__ Y2 = reinterpret_cast<bf16_t*>(p.y2);
+  const int flags = p.flags;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)smem;
+  const uint32_t lds_wave = lds0 + (uint32_t)wave * 1024u;
+
+  // BN tables (mean | inv) of every output channel, for the whole kernel
+  float* tab = reinterpret_cast<float*>(smem + GW_NST * GW_SLOT);
+  if (flags & EPI_AFFINE) {
+    for (int k = tid; k < p.coutp; k += GW_NT) {
+      tab[k] = k < p.Cout ? p.mean[k] : 0.f;
+      tab[p.coutp + k] = k < p.Cout ? p.inv[k] : 0.f;
+    }
+  }
+  __syncthreads();   // no DMA in flight yet
+
+  // ---- load side: the (tile, step) whose operands are being fetched
+  const bf16_t* src[NLMAX];
+  int l_tile = 0, l_k = 0, l_co0 = 0, l_px0 = 0;
+  auto set_load_tile = [&](int tj) {
+    const int lid = t_first + tj * t_step;
+    l_co0 = (lid % cblocks) * BN;
+    l_px0 = (lid / cblocks) * GW_BM;
+#pragma unroll
+    for (int i = 0; i < NLMAX; ++i) {
+      if (i >= NLw) break;
+      // group gi = 16 rows of the slot; lane -> row 16gi + lane/4, position lane%4
+      const int row = 16 * (wave + 8 * i) + (lane >> 2);
+      const int c = (lane & 3) ^ gw_swz(row);
+      if (row < BN) {
+        src[i] = Wt + (size_t)(l_co0 + row) * p.kp + c * 8;
+      } else {
+        // rows past M re-read pixel M-1: their outputs are never stored
+        const int pix = min(l_px0 + row - BN, M - 1);
+        const int n = pix / HoWo, rr = pix - n * HoWo;
+        const int ho = rr / p.Wo, wo = rr - ho * p.Wo;
+        src[i] = X + (((size_t)n * p.H + ho * p.sh) * p.W + wo * p.sw) * p.ldx + c * 8;
+      }
+    }
+  };
+  auto issue = [&](int slot) {
+    const uint32_t base = lds_wave + (uint32_t)slot * GW_SLOT;
+    if (l_k < KT) {
+      const int ko = l_k * 32;
+#pragma unroll
+      for (int i = 0; i < NLMAX; ++i) {
+        if (i >= NLw) break;
+        gw_glds16(src[i] + ko, base + i * 8192u);
+      }
+    } else if (RES) {
+      // residual phase ph: slot row r (512 B) = pixel l_px0 + 64(r/16) + 16 ph + r%16
+      const int ph = l_k - KT;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = 2 * (wave + 8 * i) + (lane >> 5);
+        const int c = (lane & 31) ^ (row & 15);
+        const int pix = min(l_px0 + 64 * i + 16 * ph + (row & 15), M - 1);
+        gw_glds16(R + (size_t)pix * p.ldr + l_co0 + c * 8, base + i * 8192u);
+      }
+    }
+    // advance; past the last tile the final step is re-read (never consumed)
+    if (l_k + 1 < SPT) {
+      ++l_k;
+    } else if (l_tile + 1 < ntiles) {
+      ++l_tile;
+      l_k = 0;
+      set_load_tile(l_tile);
+    }
+  };
+
+  set_load_tile(0);
+  issue(0);
+  issue(1);
+  issue(2);
+
+  f32x4 acc[NI][4];
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int cs = (g ^ gw_swz(col)) << 4;   // fragment chunk byte offset (rows 16 | base)
+  const int offa = (wm * (BN / 2) + col) * 64 + cs;
+  const int offb = (BN + wn * 64 + col) * 64 + cs;
+
+  // epilogue of 16-pixel column J for every 32-cout group (rl: residual slot or null)
+  auto epi = [&](auto jc, int co0, int px0, const char* rl) {
+    constexpr int J = decltype(jc)::value;
+    const int pix = px0 + wn * 64 + 16 * J + col;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int chl = wm * (BN / 2) + 32 * q + 8 * g;
+      const int ch = co0 + chl;
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = acc[2 * q][J][e];
+        v[4 + e] = acc[2 * q + 1][J][e];
+      }
+      if (flags & EPI_PRE_RELU) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+      }
+      if (flags & EPI_AFFINE) {
+        const f32x4 m0 = *reinterpret_cast<const f32x4*>(tab + ch);
+        const f32x4 m1 = *reinterpret_cast<const f32x4*>(tab + ch + 4);
+        const f32x4 i0 = *reinterpret_cast<const f32x4*>(tab + p.coutp + ch);
+        const f32x4 i1 = *reinterpret_cast<const f32x4*>(tab + p.coutp + ch + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = (v[e] - m0[e]) * i0[e];
+          v[4 + e] = (v[4 + e] - m1[e]) * i1[e];
+        }
+      }
+      if (RES && rl && ch < p.ysplit) {   // the dual-destination part has none
+        const int row = wn * 16 + col;
+        const bf16x8 r8 = *reinterpret_cast<const bf16x8*>(
+            rl + row * 512 + ((((chl >> 3) ^ (row & 15))) << 4));
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += (float)r8[e];
+      }
+      if (flags & EPI_RELU) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+      }
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = (bf16_t)v[e];
+      void* dst;
+      if (ch < p.Cout && pix < M)
+        dst = ch < p.ysplit ? (void*)(Y + (size_t)pix * p.ldy + ch)
+                            : (void*)(Y2 + (size_t)pix * p.ldy2 + (ch - p.ysplit));
+      else
+        dst = &g_gw_sink[lane];
+      gw_st16(dst, __builtin_bit_cast(u32x4, o));
+    }
+  };
+
+  int c_tile = 0, c_k = 0;
+  int st1 = 0, st2 = 0, st3 = 0;   // stores issued in steps s-1, s-2, s-3
+  for (int s = 0; s < S; ++s) {
+    // operands of step s landed (this wave's DMA); younger: steps s+1, s+2's
+    // DMA and the stores of the last three steps (issued after step s's DMA)
+    gw_wait_vm(2 * NLw + st1 + st2 + st3);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    issue((s + 3) & 3);
+    __builtin_amdgcn_sched_barrier(0);
+    const int lid = t_first + c_tile * t_step;
+    const int co0 = (lid % cblocks) * BN;
+    const int px0 = (lid / cblocks) * GW_BM;
+    const char* L = smem + (s & 3) * GW_SLOT;
+    int nst = 0;
+    if (c_k < KT) {
+      bf16x8 a[NI], b[4];
+#pragma unroll
+      for (int i = 0; i < NI; ++i) a[i] = *reinterpret_cast<const bf16x8*>(L + offa + i * 1024);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const bf16x8*>(L + offb + j * 1024);
+#pragma unroll
+      for (int i = 0; i < NI; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma_step(a[i], b[j], acc[i][j]);
+      if (!RES && c_k == KT - 1) {
+        epi(std::integral_constant<int, 0>{}, co0, px0, nullptr);
+        epi(std::integral_constant<int, 1>{}, co0, px0, nullptr);
+        epi(std::integral_constant<int, 2>{}, co0, px0, nullptr);
+        epi(std::integral_constant<int, 3>{}, co0, px0, nullptr);
+        nst = 4 * NQ;
+      }
+    } else if (RES) {
+      const int ph = c_k - KT;
+      if (ph == 0) epi(std::integral_constant<int, 0>{}, co0, px0, L);
+      else if (ph == 1) epi(std::integral_constant<int, 1>{}, co0, px0, L);
+      else if (ph == 2) epi(std::integral_constant<int, 2>{}, co0, px0, L);
+      else epi(std::integral_constant<int, 3>{}, co0, px0, L);
+      nst = NQ;
+    }
+    st3 = st2;
+    st2 = st1;
+    st1 = nst;
+    if (c_k + 1 == SPT) {
+#pragma unroll
+      for (int i = 0; i < NI; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      c_k = 0;
+      ++c_tile;
+    } else {
+      ++c_k;
+    }
+  }
+  // drain: the trailing (never consumed) DMA must land before the workgroup
+  // releases its LDS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// BN of the wide tile for this conv, or 0 if gemm1x1_wide does not apply
+int gemm_wide_bn(const ConvParams& p) {
+  if (p.in_mean || p.kp % 32 || p.kp / 32 < 3 || p.Cout % 8) return 0;
+  const int M = p.N * p.Ho * p.Wo;
+  int bn = 0;
+  if (p.Cout % 256 == 0) bn = 256;
+  else if (p.Cout % 192 == 0 && !(p.flags & EPI_RES)) bn = 192;
+  if (!bn || p.Cout > 2048) return 0;
+  if ((p.flags & EPI_RES) && (!p.res || p.ldr % 8)) return 0;
+  const int T = ((M + GW_BM - 1) / GW_BM) * (p.Cout / bn);
+  return T >= 8 ? bn : 0;
+}
+
+hipError_t launch_gemm_wide(const ConvParams& p0, int num_cu, hipStream_t s) {
+  const int bn = gemm_wide_bn(p0);
+  if (!bn) return hipErrorInvalidValue;
+  ConvParams p = p0;
+  p.coutp = p.Cout;   // whole BN blocks (the weights hold >= roundup128(Cout) rows)
+  const int M = p.N * p.Ho * p.Wo;
+  const int T = ((M + GW_BM - 1) / GW_BM) * (p.Cout / bn);
+  int G = num_cu < T ? num_cu : T;
+  G = G / 8 * 8;
+  const size_t lds = GW_NST * GW_SLOT + ((p.flags & EPI_AFFINE) ? 8 * (size_t)p.coutp : 0);
+  if (bn == 192)
+    hipLaunchKernelGGL((gemm1x1_wide<192, false>), dim3(G), dim3(GW_NT), lds, s, p);
+  else if (p.flags & EPI_RES)
+    hipLaunchKernelGGL((gemm1x1_wide<256, true>), dim3(G), dim3(GW_NT), lds, s, p);
+  else
+    hipLaunchKernelGGL((gemm1x1_wide<256, false>), dim3(G), dim3(GW_NT), lds, s, p);
+  return hipGetLastError();
+}
+
+}  // namespace vox
