@@ -41,7 +41,7 @@ def _kernel_name(tag, dt):
     if tag & (1 << 27):
         return "gemm1x1_pipe"
     if tag & (1 << 26):
-        return "split_s2_rows"
+        return "s2_fused" if tag & (1 << 19) else "split_s2_rows"
     if tag & (1 << 25):
         return "chain_rows"
     if tag & (1 << 24):

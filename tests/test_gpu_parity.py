@@ -201,9 +201,10 @@ def test_extract_cli_end_to_end(weights, tmp_path):
 
 @pytest.mark.parametrize("unfused_env", [("VOXEMB_NO_BNECK",), ("VOXEMB_NO_CHAIN_ROWS",),
                                          ("VOXEMB_NO_SPLIT_S2",), ("VOXEMB_NO_GEMM_PIPE",),
+                                         ("VOXEMB_NO_S2_FUSED",),
                                          ("VOXEMB_NO_BNECK", "VOXEMB_NO_CHAIN", "VOXEMB_NO_SPLIT_S2",
                                           "VOXEMB_NO_GEMM_PIPE")],
-                         ids=["chain", "tiled_chain", "split_s2", "gemm_pipe", "unfused"])
+                         ids=["chain", "tiled_chain", "split_s2", "gemm_pipe", "s2_fused", "unfused"])
 @pytest.mark.parametrize("name,F,T,N", [("res2net50_w24_s4_c32", 80, 200, 3),
                                         ("res2net50_w24_s4_c32", 80, 37, 3),
                                         ("res2net50_w24_s4_c32", 40, 75, 2),
@@ -342,3 +343,22 @@ def test_graph_replay_equals_eager(weights, name, F, T, N, monkeypatch):
         ref = [ex.run(x) for x in xs] + [ex.run(xs[0])]
     for a, b in zip(got, ref):
         assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("F,T,N", [(80, 200, 3), (80, 37, 2), (40, 75, 2), (80, 27, 1)])
+def test_s2_fused_bitwise(weights, F, T, N, monkeypatch):
+    """The fused stride-2 front half (1x1a on the full-resolution input, the
+    three 3x3/2 branches and the pool of the last split in one launch; odd and
+    tiny heights, row segments) gives the same bits as 1x1a + split_s2_rows."""
+    import torch
+    from voxsrc2020_speaker_verification_amd import synth
+    spec, t, blob = weights("res2net50_w24_s4_c32", F)
+    x = synth.make_features(N, T, F, seed=31)
+    with _extractor(blob, "bf16") as ex:
+        got = ex.run(x)
+        assert any(l.startswith("s2fused") for l in ex.describe(torch.from_numpy(x).cuda()))
+    monkeypatch.setenv("VOXEMB_NO_S2_FUSED", "1")
+    with _extractor(blob, "bf16") as ex:
+        ref = ex.run(x)
+        assert not any(l.startswith("s2fused") for l in ex.describe(torch.from_numpy(x).cuda()))
+    assert np.array_equal(got, ref)

@@ -883,6 +883,294 @@ __global__ __launch_bounds__((SplitS2Cfg<WID, S, WIN>::NT)) void split_s2_rows(C
   }
 }
 
+// ----------------------------------------------------------------------------
+// Stride-2 block front half in one launch (res2net_model.py:90-93 + 53-77,
+// layer-2 block 0): the 1x1a (+BN+ReLU) on the full-resolution block input
+// and split_s2_rows' stride-2 branches / average pool, so the 1x1a output
+// (S*w channels at full resolution, the largest tensor of the stage) never
+// touches HBM.  Output row ho needs 1x1a rows 2ho-1..2ho+1: step ho stages
+// input rows 2ho, 2ho+1 (global -> registers one step ahead -> LDS), then
+//   phase A: wave (pair pq, row rr) computes 32 1x1a channels of A-row
+//            2ho+rr for all pixels (weights in registers) -> 3-row ring;
+//   phase B: split_s2_rows' branch waves / pool waves on rows 2ho-1..2ho+1.
+// A segment starts with one warm-up step (A-rows 2g0-2, 2g0-1).  Same
+// roundings and K orders as the unfused 1x1a + split kernels: bit-identical.
+template <int CI, int WID, int S, int WIN>
+struct S2FusedCfg {
+  static constexpr int WOUT = (WIN + 1) / 2;
+  static constexpr int PTO = (WOUT + 15) / 16;   // output pixel tiles
+  static constexpr int PTI = (WIN + 15) / 16;    // input pixel tiles
+  static constexpr int WR = WIN + 2;             // ring row: pad | WIN | pad
+  static constexpr int WCO = (WID + 15) / 16;
+  static constexpr int ROLES = (S - 1) * WCO;    // branch (stage, cout tile) waves
+  static constexpr int SW = S * WID;
+  static constexpr int NPA = SW / 32;            // 1x1a channel pairs
+  static constexpr int NW = SW / 16;             // one 1x1a 16-channel tile per wave
+  static constexpr int NT = 64 * NW;
+  static constexpr int KSA = CI / 32;
+  static constexpr int KFLAT = 9 * WID;
+  static constexpr int KST = (KFLAT + 31) / 32;
+  static constexpr int AU = ((WID / 8) & 1) ? WID / 8 : WID / 8 + 1;
+  static constexpr int ASTR = AU * 16;
+  static constexpr int IU = ((CI / 8) & 1) ? CI / 8 : CI / 8 + 1;
+  static constexpr int ISTR = IU * 16;           // staged input pixel stride
+  static constexpr int ROWB = WR * ASTR, PLANEB = 3 * ROWB;
+  static constexpr int RING = S * PLANEB;
+  static constexpr int INROW = WIN * ISTR;
+  static constexpr int CU = CI / 8;
+  static constexpr int XREG = (2 * WIN * CU + NT - 1) / NT;   // two input rows per step
+  static constexpr int LDS = RING + 2 * INROW + 4 * (2 * (S - 1) * 16 * WCO + 2 * SW) + 4 * 4 * KST;
+};
+
+template <int CI, int WID, int S, int WIN>
+__global__ __launch_bounds__((S2FusedCfg<CI, WID, S, WIN>::NT)) void s2_fused(ChainParams q) {
+  using K = S2FusedCfg<CI, WID, S, WIN>;
+  constexpr int NT = K::NT, WCO = K::WCO, KST = K::KST, ASTR = K::ASTR, CU = K::CU;
+  constexpr int W = WIN, Wo = K::WOUT, ROWB = K::ROWB, PLANEB = K::PLANEB;
+  static_assert(K::NW > K::ROLES, "spare waves pool the last split");
+  static_assert(K::SW % 32 == 0 && WID % 8 == 0 && CI % 32 == 0, "shape");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int col = lane & 15, g = lane >> 4;
+  const int H = q.H;
+  const int Ho = (H + 1) / 2;
+  const int nseg = q.nwaves;
+  const int n = blockIdx.x / nseg;
+  const int g0 = (blockIdx.x - n * nseg) * q.R;
+  const int g1 = min(Ho, g0 + q.R);
+  char* rings = smem;
+  char* inb = smem + K::RING;
+  float* bmb = reinterpret_cast<float*>(inb + 2 * K::INROW);
+  float* bib = bmb + (S - 1) * 16 * WCO;
+  float* bma = bib + (S - 1) * 16 * WCO;          // 1x1a BN [SW]
+  float* bia = bma + K::SW;
+  int* ktab_l = reinterpret_cast<int*>(bia + K::SW);   // [4 lane groups][KST]
+  const bf16_t* __restrict__ X = reinterpret_cast<const bf16_t*>(q.x);
+  bf16_t* __restrict__ Bo = reinterpret_cast<bf16_t*>(q.b);
+  const size_t img = (size_t)n * H * W;
+  const size_t imgo = (size_t)n * Ho * Wo;
+
+  for (int i = tid; i < K::RING / 16; i += NT)
+    reinterpret_cast<uint4*>(rings)[i] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+  for (int k = 0; k < S - 1; ++k)
+    for (int c = tid; c < 16 * WCO; c += NT) {
+      bmb[k * 16 * WCO + c] = c < WID ? q.mean[k][c] : 0.f;
+      bib[k * 16 * WCO + c] = c < WID ? q.inv[k][c] : 0.f;
+    }
+  for (int c = tid; c < K::SW; c += NT) {
+    bma[c] = q.ma[c];
+    bia[c] = q.ia[c];
+  }
+
+  // branch role weights (registers)
+  const bool role = wave < K::ROLES;
+  const int ck = role ? wave / WCO : 0;
+  const int ci = wave % WCO;
+  bf16x8 wb[KST];
+  {
+    const void* wk = q.wt[0];
+#pragma unroll
+    for (int k = 1; k < S - 1; ++k)
+      if (ck == k) wk = q.wt[k];
+    const bf16_t* __restrict__ Wk = reinterpret_cast<const bf16_t*>(wk);
+#pragma unroll
+    for (int s = 0; s < KST; ++s) {
+      const int kk = 32 * s + 8 * g;
+      wb[s] = (role && kk < K::KFLAT) ? ld16(Wk + (size_t)(ci * 16 + col) * K::KFLAT + kk)
+                                      : bf16x8{};
+    }
+  }
+  // 1x1a: one 16-row tile t of the paired-row weights per wave, for both
+  // staged rows; lane (col, g) gets channels 32(t/2) + 8g + 4(t%2) + 0..3
+  const int t16 = wave;
+  bf16x8 w1[K::KSA];
+  {
+    const bf16_t* __restrict__ Wa = reinterpret_cast<const bf16_t*>(q.wa);
+#pragma unroll
+    for (int s = 0; s < K::KSA; ++s)
+      w1[s] = ld16(Wa + (size_t)(t16 * 16 + col) * CI + 32 * s + 8 * g);
+  }
+  for (int i = tid; i < 4 * KST; i += NT) {
+    const int gg = i / KST, s = i - gg * KST;
+    const int kk = 32 * s + 8 * gg;
+    int dyi = 1, off = 0;
+    if (kk < K::KFLAT) {
+      const int tap = kk / WID, ch = kk - tap * WID;
+      dyi = tap / 3;
+      off = (tap % 3 - 1) * ASTR + ch * 2;
+    }
+    ktab_l[i] = (dyi << 24) | (off + 32768);
+  }
+
+  // two input rows per step: global -> registers (one step ahead) -> LDS
+  uint4 xr[K::XREG];
+  const int ldx = q.ldx;
+  auto load_x = [&](int r0) __attribute__((always_inline)) {
+    const bf16_t* base = X + (img + (size_t)r0 * W) * ldx;
+#pragma unroll
+    for (int i = 0; i < K::XREG; ++i) {
+      int c = tid + i * NT;
+      asm volatile("" : "+v"(c));   // recomputed per step: nothing hoisted into registers
+      const int rr = c / (W * CU), cc = c - rr * (W * CU);
+      const int px = cc / CU, u = cc - px * CU;
+      const int r = r0 + rr;
+      xr[i] = make_uint4(0, 0, 0, 0);
+      if (rr < 2 && r >= 0 && r < H)
+        xr[i] = *reinterpret_cast<const uint4*>(base + (rr * W + px) * ldx + u * 8);
+    }
+  };
+  auto store_x = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < K::XREG; ++i) {
+      int c = tid + i * NT;
+      asm volatile("" : "+v"(c));
+      const int rr = c / (W * CU), cc = c - rr * (W * CU);
+      const int px = cc / CU, u = cc - px * CU;
+      if (rr < 2) *reinterpret_cast<uint4*>(inb + rr * K::INROW + px * K::ISTR + u * 16) = xr[i];
+    }
+  };
+
+  load_x(2 * (g0 - 1));
+  store_x();
+  __syncthreads();
+  for (int ho = g0 - 1; ho < g1; ++ho) {
+    load_x(2 * ho + 2);   // lands during this step, goes to LDS at its end
+    // ---------------- phase A: 1x1a rows 2ho, 2ho+1 -> ring
+    {
+      const int ch = 32 * (t16 >> 1) + 8 * g + 4 * (t16 & 1);
+      const int p = ch / WID, off = ch - p * WID;
+      const f32x4 m0 = *reinterpret_cast<const f32x4*>(bma + ch);
+      const f32x4 i0 = *reinterpret_cast<const f32x4*>(bia + ch);
+#pragma unroll
+      for (int rr = 0; rr < 2; ++rr) {
+        const int r = 2 * ho + rr;
+        const bool inimg = r >= 0 && r < H;
+        char* dst = rings + p * PLANEB + ((r + 840) % 3) * ROWB + off * 2;
+        const char* src = inb + rr * K::INROW + (8 * g) * 2;
+#pragma unroll
+        for (int j = 0; j < K::PTI; ++j) {
+          const int px = 16 * j + col;
+          const int pr = px < W ? px : W - 1;
+          bf16x8 b[K::KSA];
+#pragma unroll
+          for (int s = 0; s < K::KSA; ++s)
+            b[s] = *reinterpret_cast<const bf16x8*>(src + pr * K::ISTR + 64 * s);
+          f32x4 a0 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int s = 0; s < K::KSA; ++s) a0 = mfma_step(w1[s], b[s], a0);
+          bf16x4 o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = (bf16_t)fmaxf((a0[e] - m0[e]) * i0[e], 0.f);
+          if (!inimg) o = bf16x4{};   // the fixed zero padding of the stride-2 convs
+          if (px < W) *reinterpret_cast<bf16x4*>(dst + (px + 1) * ASTR) = o;
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    }
+    __syncthreads();
+    // ---------------- phase B: output row ho from A-rows 2ho-1 .. 2ho+1
+    if (ho >= g0) {
+      const int rb0 = __builtin_amdgcn_readfirstlane(((2 * ho - 1 + 840) % 3) * ROWB);
+      const int rb1 = __builtin_amdgcn_readfirstlane(((2 * ho + 840) % 3) * ROWB);
+      const int rb2 = __builtin_amdgcn_readfirstlane(((2 * ho + 1 + 840) % 3) * ROWB);
+      if (role) {
+        const int co = 16 * ci + 4 * g;
+        const char* zb = rings + ck * PLANEB;
+        const f32x4 m = *reinterpret_cast<const f32x4*>(bmb + ck * 16 * WCO + co);
+        const f32x4 sc = *reinterpret_cast<const f32x4*>(bib + ck * 16 * WCO + co);
+        int boff[KST];
+#pragma unroll
+        for (int s = 0; s < KST; ++s) {
+          int e = ktab_l[g * KST + s];
+          const int dyi = e >> 24;
+          boff[s] = (dyi == 0 ? rb0 : (dyi == 1 ? rb1 : rb2)) + (e & 0xFFFFFF) - 32768 + ASTR;
+        }
+#pragma unroll 1
+        for (int j = 0; j < K::PTO; ++j) {
+          const int wo = 16 * j + col;
+          const int wr = 2 * (wo < Wo ? wo : Wo - 1) * ASTR;
+          f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+          constexpr int KH = (KST + 2) / 3;   // B fragments in thirds (register budget)
+#pragma unroll
+          for (int h = 0; h < 3; ++h) {
+            bf16x8 b0[KH];
+#pragma unroll
+            for (int i = 0; i < KH; ++i)
+              if (h * KH + i < KST)
+                b0[i] = *reinterpret_cast<const bf16x8*>(zb + boff[h * KH + i] + wr);
+#pragma unroll
+            for (int i = 0; i < KH; ++i)
+              if (h * KH + i < KST) acc = mfma_step(wb[h * KH + i], b0[i], acc);
+            __builtin_amdgcn_sched_barrier(0);   // one third of the fragments live at a time
+          }
+          if (co < WID && wo < Wo) {
+            bf16x4 y;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) y[e] = (bf16_t)fmaxf((acc[e] - m[e]) * sc[e], 0.f);
+            *reinterpret_cast<bf16x4*>(Bo + (imgo + (size_t)ho * Wo + wo) * q.ldb + ck * WID + co) = y;
+          }
+        }
+      } else {
+        // last split: AvgPool 3x3/2 VALID over the fixed-padded plane, divisor 9
+        // (taps outside the image skipped, in the order of avgpool3s2_v8)
+        const char* pl = rings + (S - 1) * PLANEB;
+        const int st = tid - 64 * K::ROLES, nst = NT - 64 * K::ROLES;
+        for (int it = st; it < Wo * (WID / 8); it += nst) {
+          const int wo = it / (WID / 8), u = it - wo * (WID / 8);
+          float sum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int ky = 0; ky < 3; ++ky) {
+            const int hi = 2 * ho - 1 + ky;
+            if (hi < 0 || hi >= H) continue;
+            const int rb = ky == 0 ? rb0 : (ky == 1 ? rb1 : rb2);
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx) {
+              const int wi = 2 * wo - 1 + kx;
+              if (wi < 0 || wi >= W) continue;
+              const bf16x8 v = *reinterpret_cast<const bf16x8*>(pl + rb + (wi + 1) * ASTR + u * 16);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) sum[e] += (float)v[e];
+            }
+          }
+          bf16x8 o;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = (bf16_t)(sum[e] / 9.0f);
+          *reinterpret_cast<bf16x8*>(Bo + (imgo + (size_t)ho * Wo + wo) * q.ldb + (S - 1) * WID + u * 8) = o;
+        }
+      }
+    }
+    store_x();   // input rows 2ho+2, 2ho+3 (phase A of this step is done with the staging)
+    __syncthreads();
+  }
+}
+
+#define S2_FUSED_SHAPES(X) \
+  X(128, 48, 4, 80)  /* res2net50_w24_s4_c32 layer-2 block 0, 80-d features */ \
+  X(128, 48, 4, 40)  /* ... 40-d features */
+
+int s2_fused_lds(int ci, int wid, int s, int W) {
+#define X_LDS(ci_, w_, s_, win_) \
+  if (ci == ci_ && wid == w_ && s == s_ && W == win_) return S2FusedCfg<ci_, w_, s_, win_>::LDS;
+  S2_FUSED_SHAPES(X_LDS)
+#undef X_LDS
+  return -1;
+}
+
+hipError_t launch_s2_fused(const ChainParams& q, hipStream_t st) {
+#define X_LAUNCH(ci_, w_, s_, win_)                                                      \
+  if (q.cin == ci_ && q.w == w_ && q.nst + 1 == s_ && q.W == win_) {                      \
+    using K = S2FusedCfg<ci_, w_, s_, win_>;                                              \
+    hipLaunchKernelGGL((s2_fused<ci_, w_, s_, win_>), dim3(q.N * q.nwaves), dim3(K::NT),  \
+                       K::LDS, st, q);                                                    \
+    return hipGetLastError();                                                             \
+  }
+  S2_FUSED_SHAPES(X_LAUNCH)
+#undef X_LAUNCH
+  return hipErrorInvalidValue;
+}
+
 #define SPLIT_S2_SHAPES(X) \
   X(48, 4, 80)  /* res2net50_w24_s4_c32 layer-2 block 0, 80-d features */ \
   X(48, 4, 40)  /* ... 40-d features */

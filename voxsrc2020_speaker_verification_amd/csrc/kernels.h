@@ -58,6 +58,9 @@ struct ChainParams {
   int N, H, W, w, nst, R, coutp;
   int astr, wstr, kcp, buf_bytes, lds;
   int nwaves;                       // 4 or 8 waves per block
+  // s2_fused only: the block input and its 1x1a (paired-row weights + BN)
+  const void* x; int ldx; int cin;
+  const void* wa; const float* ma; const float* ia;
 };
 hipError_t launch_split_chain(const ChainParams& q, int wco, int wpx, hipStream_t s);
 // Row-streamed split chain (bneck.hip): utterance segments of q.R rows, q.nwaves
@@ -69,6 +72,11 @@ hipError_t launch_chain_rows(const ChainParams& q, hipStream_t s);
 // segments per utterance; q.H/q.W are the INPUT dims.  LDS bytes or -1.
 int split_s2_lds(int w, int split, int W);
 hipError_t launch_split_s2(const ChainParams& q, hipStream_t s);
+// Stride-2 block front half (bneck.hip): 1x1a + BN + ReLU on the full-res
+// input q.x (q.cin channels, weights q.wa) feeding split_s2_rows' branches and
+// pool in the same launch; q.H/q.W are the INPUT dims.  LDS bytes or -1.
+int s2_fused_lds(int cin, int wid, int split, int W);
+hipError_t launch_s2_fused(const ChainParams& q, hipStream_t s);
 
 // Fused Res2Net bottleneck (stride 1): 1x1a + split chain + 1x1c + identity
 // or 1x1-projection shortcut in one launch, intermediates in LDS ring
