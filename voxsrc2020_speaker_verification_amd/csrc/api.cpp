@@ -1331,7 +1331,7 @@ static hipError_t run_op(vox_model* m, const Op& op, hipStream_t s) {
     case 18: return launch_gemm_pipe(op.cp, m->num_cu, m->gemm_var, s);
     case 19: return launch_gconv(op.gq, s);
     case 20: return launch_conv3_pipe(op.cp, m->num_cu, s);
-    case 21: return launch_gemm_wide(op.cp, m->num_cu, s);
+    case 21: return launch_gemm_wide(op.cp, m->num_cu, m->gemm_var, s);
     case 10: return launch_split_chain(op.ch, op.cl.wco, op.cl.wpx, s);
     case 12: return launch_bneck(op.bq, op.cin, op.C, op.cl.wco, op.S, s);
     case 13: return launch_chain_rows(op.ch, s);

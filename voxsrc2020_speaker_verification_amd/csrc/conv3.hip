@@ -248,21 +248,30 @@ void conv3x3_pipe(ConvParams p) {
     }
     __builtin_amdgcn_sched_barrier(0);
     const char* L = smem + (s % C3_NST) * C3_SLOT;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    {
+      // both half-steps' fragments are read before the first MFMA (the LDS
+      // latency exposed once per step, counted lgkmcnt waits in issue order);
       // the all-zero half-step past K (K % 64 == 32) is skipped, as in the
       // generic path's K loop
-      if (ks == 1 && (K % 64) != 0 && last) break;
-      const int cs = ((ks * 4 + g) ^ swa) << 4;
-      bf16x8 a[6], b[2];
+      const bool two = !((K % 64) != 0 && last);
+      bf16x8 a[2][6], b[2][2];
 #pragma unroll
-      for (int i = 0; i < 6; ++i) a[i] = *reinterpret_cast<const bf16x8*>(L + offa[i] + cs);
+      for (int ks = 0; ks < 2; ++ks) {
+        const int cs = ((ks * 4 + g) ^ swa) << 4;
 #pragma unroll
-      for (int j = 0; j < 2; ++j) b[j] = *reinterpret_cast<const bf16x8*>(L + offb[j] + cs);
+        for (int j = 0; j < 2; ++j) b[ks][j] = *reinterpret_cast<const bf16x8*>(L + offb[j] + cs);
 #pragma unroll
-      for (int i = 0; i < 6; ++i)
+        for (int i = 0; i < 6; ++i) a[ks][i] = *reinterpret_cast<const bf16x8*>(L + offa[i] + cs);
+      }
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = mfma_step(a[i], b[j], acc[i][j]);
+      for (int ks = 0; ks < 2; ++ks) {
+        if (ks == 1 && !two) break;
+#pragma unroll
+        for (int i = 0; i < 6; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][j] = mfma_step(a[ks][i], b[ks][j], acc[i][j]);
+      }
     }
     ++epi_age;
     if (last) {

@@ -309,21 +309,45 @@ void gemm1x1_pipe(ConvParams p) {
     __builtin_amdgcn_sched_barrier(0);
     const int sb = (s % GP_NST) * GP_SLOT;
     const char* L = smem + sb;
+    if (PRO) {   // (register budget: the prologue variant reads per half step)
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      if (DBG == 1) break;
-      if (PRO && ks == 1 && last && (p.kp & 63)) break;   // zero half step past kp
-      const int cs = ((ks * 4 + g) ^ swa) << 4;
-      bf16x8 a[4], b[4];
+      for (int ks = 0; ks < 2; ++ks) {
+        if (ks == 1 && last && (p.kp & 63)) break;   // zero half step past kp
+        const int cs = ((ks * 4 + g) ^ swa) << 4;
+        bf16x8 a[4], b[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        a[i] = *reinterpret_cast<const bf16x8*>(L + offa[i] + cs);
-        b[i] = *reinterpret_cast<const bf16x8*>(L + offb[i] + cs);
+        for (int i = 0; i < 4; ++i) {
+          a[i] = *reinterpret_cast<const bf16x8*>(L + offa[i] + cs);
+          b[i] = *reinterpret_cast<const bf16x8*>(L + offb[i] + cs);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = mfma_step(a[i], b[j], acc[i][j]);
       }
+    } else if (DBG != 1) {
+      // both half-steps' fragments are read before the first MFMA (the LDS
+      // latency exposed once per step, counted lgkmcnt waits in issue order)
+      const bool two = true;
+      bf16x8 a[2][4], b[2][4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int ks = 0; ks < 2; ++ks) {
+        const int cs = ((ks * 4 + g) ^ swa) << 4;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mfma_step(a[i], b[j], acc[i][j]);
+        for (int i = 0; i < 4; ++i) {
+          b[ks][i] = *reinterpret_cast<const bf16x8*>(L + offb[i] + cs);
+          a[ks][i] = *reinterpret_cast<const bf16x8*>(L + offa[i] + cs);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        if (ks == 1 && !two) break;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = mfma_step(a[ks][i], b[ks][j], acc[i][j]);
+      }
     }
     ++epi_age;
     if (last) {

@@ -85,7 +85,9 @@ __device__ __forceinline__ int gw_swz(int r) { return (4 - ((r >> 2) & 3)) & 3; 
 __device__ uint4 g_gw_sink[64];   // destination of masked lanes' stores
 
 #pragma clang fp contract(off)
-template <int BN, bool RES>
+// DBG (diagnostics only, VOXEMB_GEMM_VAR): 1 = no MFMA / fragment reads,
+// 2 = no operand DMA, 4 = no output stores; results are garbage
+template <int BN, bool RES, int DBG = 0>
 __global__ __launch_bounds__(GW_NT) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void gemm1x1_wide(ConvParams p) {
   constexpr int NI = BN / 32;                // 16-cout MFMA blocks per wave (BN/2 couts)
@@ -172,27 +174,22 @@ void gemm1x1_wide(ConvParams p) {
       }
     }
   };
-  auto issue = [&](int slot) {
-    const uint32_t base = lds_wave + (uint32_t)slot * GW_SLOT;
+  // DMA piece i (1 KB per wave) of the step being fetched into ring slot `slot`
+  auto issue_piece = [&](int slot, int i) {
+    const uint32_t base = lds_wave + (uint32_t)slot * GW_SLOT + (uint32_t)i * 8192u;
     if (l_k < KT) {
-      const int ko = l_k * 32;
-#pragma unroll
-      for (int i = 0; i < NLMAX; ++i) {
-        if (i >= NLw) break;
-        gw_glds16(src[i] + ko, base + i * 8192u);
-      }
+      if (i < NLw && !(DBG & 2)) gw_glds16(src[i] + l_k * 32, base);
     } else if (RES) {
       // residual phase ph: slot row r (512 B) = pixel l_px0 + 64(r/16) + 16 ph + r%16
       const int ph = l_k - KT;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = 2 * (wave + 8 * i) + (lane >> 5);
-        const int c = (lane & 31) ^ (row & 15);
-        const int pix = min(l_px0 + 64 * i + 16 * ph + (row & 15), M - 1);
-        gw_glds16(R + (size_t)pix * p.ldr + l_co0 + c * 8, base + i * 8192u);
-      }
+      const int row = 2 * (wave + 8 * i) + (lane >> 5);
+      const int c = (lane & 31) ^ (row & 15);
+      const int pix = min(l_px0 + 64 * i + 16 * ph + (row & 15), M - 1);
+      gw_glds16(R + (size_t)pix * p.ldr + l_co0 + c * 8, base);
     }
-    // advance; past the last tile the final step is re-read (never consumed)
+  };
+  // advance; past the last tile the final step is re-read (never consumed)
+  auto advance = [&]() {
     if (l_k + 1 < SPT) {
       ++l_k;
     } else if (l_tile + 1 < ntiles) {
@@ -200,6 +197,11 @@ void gemm1x1_wide(ConvParams p) {
       l_k = 0;
       set_load_tile(l_tile);
     }
+  };
+  auto issue = [&](int slot) {
+#pragma unroll
+    for (int i = 0; i < NLMAX; ++i) issue_piece(slot, i);
+    advance();
   };
 
   set_load_tile(0);
@@ -266,7 +268,7 @@ void gemm1x1_wide(ConvParams p) {
                             : (void*)(Y2 + (size_t)pix * p.ldy2 + (ch - p.ysplit));
       else
         dst = &g_gw_sink[lane];
-      gw_st16(dst, __builtin_bit_cast(u32x4, o));
+      if (!(DBG & 4)) gw_st16(dst, __builtin_bit_cast(u32x4, o));
     }
   };
 
@@ -278,6 +280,9 @@ void gemm1x1_wide(ConvParams p) {
     gw_wait_vm(2 * NLw + st1 + st2 + st3);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
+    // the next DMA goes into the slot every wave released at this barrier, as
+    // early as possible (measured: spreading its pieces between the MFMA row
+    // blocks is 6 % slower -- the stream is latency-bound, not issue-bound)
     issue((s + 3) & 3);
     __builtin_amdgcn_sched_barrier(0);
     const int lid = t_first + c_tile * t_step;
@@ -285,12 +290,18 @@ void gemm1x1_wide(ConvParams p) {
     const int px0 = (lid / cblocks) * GW_BM;
     const char* L = smem + (s & 3) * GW_SLOT;
     int nst = 0;
-    if (c_k < KT) {
+    if (c_k < KT && (DBG & 1)) {
+      if (!RES && c_k == KT - 1) nst = (DBG & 4) ? 0 : 4 * NQ;
+    } else if (c_k < KT) {
+      // every fragment read of the step is issued before the first MFMA, so the
+      // LDS latency is exposed once per step (counted lgkmcnt waits follow the
+      // issue order), not once per MFMA group
       bf16x8 a[NI], b[4];
 #pragma unroll
-      for (int i = 0; i < NI; ++i) a[i] = *reinterpret_cast<const bf16x8*>(L + offa + i * 1024);
-#pragma unroll
       for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const bf16x8*>(L + offb + j * 1024);
+#pragma unroll
+      for (int i = 0; i < NI; ++i) a[i] = *reinterpret_cast<const bf16x8*>(L + offa + i * 1024);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < NI; ++i)
 #pragma unroll
@@ -300,7 +311,7 @@ void gemm1x1_wide(ConvParams p) {
         epi(std::integral_constant<int, 1>{}, co0, px0, nullptr);
         epi(std::integral_constant<int, 2>{}, co0, px0, nullptr);
         epi(std::integral_constant<int, 3>{}, co0, px0, nullptr);
-        nst = 4 * NQ;
+        nst = (DBG & 4) ? 0 : 4 * NQ;
       }
     } else if (RES) {
       const int ph = c_k - KT;
@@ -308,7 +319,7 @@ void gemm1x1_wide(ConvParams p) {
       else if (ph == 1) epi(std::integral_constant<int, 1>{}, co0, px0, L);
       else if (ph == 2) epi(std::integral_constant<int, 2>{}, co0, px0, L);
       else epi(std::integral_constant<int, 3>{}, co0, px0, L);
-      nst = NQ;
+      nst = (DBG & 4) ? 0 : NQ;
     }
     st3 = st2;
     st2 = st1;
@@ -342,7 +353,17 @@ int gemm_wide_bn(const ConvParams& p) {
   return T >= 8 ? bn : 0;
 }
 
-hipError_t launch_gemm_wide(const ConvParams& p0, int num_cu, hipStream_t s) {
+template <int DBG>
+static void launch_wide_t(const ConvParams& p, int bn, int G, size_t lds, hipStream_t s) {
+  if (bn == 192)
+    hipLaunchKernelGGL((gemm1x1_wide<192, false, DBG>), dim3(G), dim3(GW_NT), lds, s, p);
+  else if (p.flags & EPI_RES)
+    hipLaunchKernelGGL((gemm1x1_wide<256, true, DBG>), dim3(G), dim3(GW_NT), lds, s, p);
+  else
+    hipLaunchKernelGGL((gemm1x1_wide<256, false, DBG>), dim3(G), dim3(GW_NT), lds, s, p);
+}
+
+hipError_t launch_gemm_wide(const ConvParams& p0, int num_cu, int variant, hipStream_t s) {
   const int bn = gemm_wide_bn(p0);
   if (!bn) return hipErrorInvalidValue;
   ConvParams p = p0;
@@ -352,12 +373,15 @@ hipError_t launch_gemm_wide(const ConvParams& p0, int num_cu, hipStream_t s) {
   int G = num_cu < T ? num_cu : T;
   G = G / 8 * 8;
   const size_t lds = GW_NST * GW_SLOT + ((p.flags & EPI_AFFINE) ? 8 * (size_t)p.coutp : 0);
-  if (bn == 192)
-    hipLaunchKernelGGL((gemm1x1_wide<192, false>), dim3(G), dim3(GW_NT), lds, s, p);
-  else if (p.flags & EPI_RES)
-    hipLaunchKernelGGL((gemm1x1_wide<256, true>), dim3(G), dim3(GW_NT), lds, s, p);
-  else
-    hipLaunchKernelGGL((gemm1x1_wide<256, false>), dim3(G), dim3(GW_NT), lds, s, p);
+  switch (variant) {   // 0 = the product kernel; 11..17 = diagnostics (DBG = variant - 10)
+    case 11: launch_wide_t<1>(p, bn, G, lds, s); break;
+    case 12: launch_wide_t<2>(p, bn, G, lds, s); break;
+    case 14: launch_wide_t<4>(p, bn, G, lds, s); break;
+    case 13: launch_wide_t<3>(p, bn, G, lds, s); break;
+    case 16: launch_wide_t<6>(p, bn, G, lds, s); break;
+    case 15: launch_wide_t<5>(p, bn, G, lds, s); break;
+    default: launch_wide_t<0>(p, bn, G, lds, s); break;
+  }
   return hipGetLastError();
 }
 

@@ -120,7 +120,7 @@ hipError_t launch_gemm_pipe(const ConvParams& p, int num_cu, int variant, hipStr
 // or 192 (Cout % 192 == 0, no residual), K % 32 == 0, K >= 96, no prologue.
 // gemm_wide_bn returns BN or 0 when it does not apply.
 int gemm_wide_bn(const ConvParams& p);
-hipError_t launch_gemm_wide(const ConvParams& p, int num_cu, hipStream_t s);
+hipError_t launch_gemm_wide(const ConvParams& p, int num_cu, int variant, hipStream_t s);
 // Persistent LDS-DMA pipelined 3x3 implicit GEMM (conv3.hip) for the Res2Net
 // branch convs with Cin in {96, 192}: stride 1 (SAME) or 2 (fixed pad 1),
 // Cout % 96 == 0, epilogue BN + ReLU; with y2 set (stride 1) it also writes
