@@ -106,6 +106,40 @@ int vox_stats_pool_device(const void* d_x, int dtype, int n, int h, int w, int c
 int vox_asnorm_stats(const float* d_trial, int n, const float* d_cohort, int m, int d,
                      int topk, float* d_mean, float* d_std, void* stream);
 
+/* ---- front end on the device: wav -> FBANK -> sliding CMN ---------------
+ * Kaldi `compute-fbank-feats` options (conf/fbank80.conf sets only
+ * sample_frequency 16000 and num_mel_bins 80; prepare_data.sh:66-70).
+ * Fixed as Kaldi's defaults: povey window, snip_edges, padded FFT (256 or 512),
+ * no energy term, log power mel energies floored at FLT_EPSILON. */
+typedef struct vox_fbank_opts {
+  float sample_frequency;         /* 16000 */
+  float frame_length_ms;          /* 25 */
+  float frame_shift_ms;           /* 10 */
+  float dither;                   /* Kaldi default 1.0 (random); 0 = deterministic */
+  float preemphasis_coefficient;  /* 0.97 */
+  int remove_dc_offset;           /* 1 */
+  int num_mel_bins;               /* Kaldi default 23; 80 / 40 in conf/fbank{80,40}.conf */
+  float low_freq;                 /* 20 */
+  float high_freq;                /* 0: Nyquist (negative: offset from Nyquist) */
+  uint64_t seed;                  /* dither noise = f(seed, frame index, sample index) */
+} vox_fbank_opts;
+void vox_fbank_default_opts(vox_fbank_opts* o);
+/* Frames of an utterance of num_samples samples (snip_edges), or < 0. */
+int64_t vox_fbank_num_frames(int64_t num_samples, const vox_fbank_opts* o);
+/* n_utt waveforms concatenated in d_wav (float sample values as Kaldi reads
+ * int16 wavs); d_samp_off / d_frame_off: device int64[n_utt + 1] prefix offsets
+ * of samples / frames (frames from vox_fbank_num_frames).  Writes
+ * d_out[total_frames][num_mel_bins] float32.  Asynchronous on `stream`.
+ * Replaces compute-fbank-feats (Kaldi feature-fbank.cc, not vendored). */
+int vox_fbank_device(const float* d_wav, const int64_t* d_samp_off, const int64_t* d_frame_off,
+                     int n_utt, int64_t total_frames, const vox_fbank_opts* o, float* d_out,
+                     void* stream);
+/* Sliding-window CMN of n_utt feature matrices [frames][f] concatenated in
+ * d_in (frame offsets d_frame_off[n_utt + 1]); bit-identical to
+ * vox_sliding_cmn per utterance.  Replaces `apply-cmvn-sliding` (tf_extract.py:63). */
+int vox_sliding_cmn_device(const float* d_in, const int64_t* d_frame_off, int n_utt, int f,
+                           int cmn_window, int center, float* d_out, void* stream);
+
 const char* vox_last_error(void);
 
 /* ---- host-side Kaldi I/O (no Kaldi binaries needed) --------------------- */

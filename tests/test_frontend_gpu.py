@@ -1,0 +1,137 @@
+"""GPU front end (csrc/fbank.hip) against the FBANK oracle (oracle/fbank_ref.py,
+Kaldi's algorithm restated; parity unpinned against Kaldi itself, which is
+absent), the device sliding CMN against the host one (bit-exact), and
+wav -> embedding on the device against the host-side composition."""
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+# float32 FFT / sums (the kernel, like Kaldi) vs the float64 restatement:
+# float32 rounding leaks ~1e-7 of a frame's largest spectral component into
+# every bin, so mel energies agree to a fraction of the frame's largest mel
+# energy (1e-5 here), and log-mel values to 1e-3 wherever a bin holds at least
+# 1e-3 of that maximum (noise-like audio: every bin)
+ENERGY_RTOL_FRAME = 1e-5
+LOGMEL_ATOL = 1e-3
+
+
+def _check_logmel(got, ref):
+    eg, er = np.exp(got.astype(np.float64)), np.exp(ref.astype(np.float64))
+    peak = er.max(1, keepdims=True)
+    assert np.all(np.abs(eg - er) <= ENERGY_RTOL_FRAME * peak + 1e-12)
+    strong = er >= 1e-3 * peak
+    assert np.all(np.abs(got - ref)[strong] <= LOGMEL_ATOL)
+
+
+def _waves(rng, lens, amp=2000.0):
+    return [(amp * rng.standard_normal(n)).astype(np.float32).round() for n in lens]
+
+
+@pytest.mark.parametrize("sr,bins", [(16000, 80), (16000, 40), (8000, 23)])
+def test_fbank_matches_oracle(sr, bins):
+    from oracle import fbank_ref
+    from voxsrc2020_speaker_verification_amd import frontend
+    rng = np.random.default_rng(bins)
+    flen, fsh = sr // 40, sr // 100
+    lens = [0, flen - 1, flen, flen + fsh, 3 * sr + 17, 1234, 2 * sr]
+    waves = _waves(rng, lens)
+    waves.append(np.zeros(5 * fsh + flen, np.float32))          # silence: log(FLT_EPSILON)
+    waves.append((np.sin(np.arange(sr) * 2 * np.pi * 440 / sr) * 10000).astype(np.float32))
+    o = frontend.FbankOptions(sample_frequency=sr, num_mel_bins=bins, dither=0.0)
+    got = frontend.fbank(waves, o, device=0)
+    nfft = 512 if flen > 256 else 256
+    for w, g in zip(waves, got):
+        ref = fbank_ref.fbank(w, bins, samp_freq=sr, frame_length=flen, frame_shift=fsh, padded=nfft)
+        assert g.shape == ref.shape
+        if ref.size:
+            _check_logmel(g, ref)
+    # silence: every energy floored at FLT_EPSILON (log within an ULP of numpy's)
+    assert np.all(got[-2] == got[-2].flat[0])
+    assert abs(float(got[-2].flat[0]) - float(np.log(np.finfo(np.float32).eps))) < 1e-5
+
+
+def test_fbank_dither_deterministic():
+    from voxsrc2020_speaker_verification_amd import frontend
+    w = _waves(np.random.default_rng(1), [8000])
+    o = frontend.FbankOptions(dither=1.0, seed=7)
+    a = frontend.fbank(w, o)[0]
+    b = frontend.fbank(w + w, o)[1]                  # batch position does not matter
+    c = frontend.fbank(w, frontend.FbankOptions(dither=1.0, seed=8))[0]
+    d = frontend.fbank(w, frontend.FbankOptions(dither=0.0))[0]
+    assert np.array_equal(a, b)
+    assert not np.array_equal(a, c) and not np.array_equal(a, d)
+    assert np.abs(a - d).max() < 0.05               # unit-variance noise on ~2000-amplitude audio
+
+
+@pytest.mark.parametrize("T", [1, 50, 300, 301, 1000, 2345])
+def test_cmn_device_bit_exact(T):
+    import torch
+    from voxsrc2020_speaker_verification_amd import frontend, kaldi
+    rng = np.random.default_rng(T)
+    mats = [rng.standard_normal((T, 80)).astype(np.float32) * 3 + 5,
+            rng.standard_normal((max(T // 3, 1), 80)).astype(np.float32)]
+    fo = np.array([0, mats[0].shape[0], mats[0].shape[0] + mats[1].shape[0]], np.int64)
+    feats = torch.from_numpy(np.concatenate(mats)).cuda()
+    out = frontend.sliding_cmn_device(feats, fo).cpu().numpy()
+    for i, m in enumerate(mats):
+        assert np.array_equal(out[fo[i]:fo[i + 1]], kaldi.sliding_cmn(m))
+
+
+def test_embed_wavs_device_equals_host_composition(weights):
+    """wav -> fbank -> CMN -> chunked embedding with features resident on the
+    device == the same kernels composed through host copies (bitwise)."""
+    from voxsrc2020_speaker_verification_amd import frontend, kaldi
+    from voxsrc2020_speaker_verification_amd.extract import embed_utterances
+    from voxsrc2020_speaker_verification_amd.extractor import Extractor
+    spec, t, blob = weights("res2net50_w24_s4_c32", 80)
+    rng = np.random.default_rng(5)
+    # 198 frames, 31 frames, 1098 frames (two chunks: 1000 + 98)
+    waves = _waves(rng, [16000 * 2 + 123, 400 + 160 * 30, 16000 * 11])
+    o = frontend.FbankOptions(dither=0.0)
+    with Extractor(blob, device=0, precision="bf16") as ex:
+        got = frontend.embed_wavs(ex, waves, o, batch=2)
+        feats = [kaldi.sliding_cmn(f) for f in frontend.fbank(waves, o)]
+        ref = embed_utterances([(str(i), f) for i, f in enumerate(feats)], ex.run, ex.dim, 2)
+    assert np.array_equal(got, ref)
+
+
+def test_wav_to_embedding_vs_oracle(weights):
+    """fp32 end to end from the waveform: GPU front end + backbone vs the
+    oracles (FBANK restatement, Kaldi CMN restatement, numpy model)."""
+    from oracle import fbank_ref, kaldi_ref, models_ref
+    from voxsrc2020_speaker_verification_amd import frontend
+    from voxsrc2020_speaker_verification_amd.extractor import Extractor
+    spec, t, blob = weights("tdnn", 40)
+    rng = np.random.default_rng(9)
+    waves = _waves(rng, [16000 * 3 + 5])
+    o = frontend.FbankOptions(num_mel_bins=40, dither=0.0)
+    with Extractor(blob, device=0, precision="fp32") as ex:
+        got = frontend.embed_wavs(ex, waves, o)
+    f = kaldi_ref.sliding_cmn(fbank_ref.fbank(waves[0], 40))
+    ref = models_ref.embed_utterance(spec, t, f)
+    assert np.abs(got[0] - ref).max() <= 2e-3 * np.abs(ref).max()
+
+
+def test_fbank_cli(tmp_path):
+    from voxsrc2020_speaker_verification_amd import frontend, kaldi
+    rng = np.random.default_rng(3)
+    waves = _waves(rng, [5000, 16000])
+    lines = []
+    for i, w in enumerate(waves):
+        p = str(tmp_path / f"u{i}.wav")
+        frontend.write_wav(p, w)
+        lines.append(f"utt{i} {p}")
+    (tmp_path / "wav.scp").write_text("\n".join(lines) + "\n")
+    conf = tmp_path / "fbank80.conf"
+    conf.write_text("--sample-frequency=16000\n--num-mel-bins=80\n")
+    ark, scp = str(tmp_path / "f.ark"), str(tmp_path / "f.scp")
+    assert frontend.main(["--config", str(conf), "--dither", "0", f"scp:{tmp_path}/wav.scp",
+                          f"ark,scp:{ark},{scp}"]) == 0
+    got = dict(kaldi.read_mat_ark(ark))
+    exp = frontend.fbank(waves, frontend.FbankOptions(dither=0.0))
+    for i in range(2):
+        assert np.array_equal(got[f"utt{i}"], exp[i])
+    items = list(kaldi.iter_features(scp, cmn=False))
+    assert [k for k, _ in items] == ["utt0", "utt1"]

@@ -26,6 +26,18 @@ VOX_BF16 = 1
 # (name, restype, argtypes) -- must mirror include/voxemb.h
 _P = C.c_void_p
 _F = C.POINTER(C.c_float)
+
+
+class FbankOpts(C.Structure):
+    """vox_fbank_opts (include/voxemb.h)."""
+    _fields_ = [("sample_frequency", C.c_float), ("frame_length_ms", C.c_float),
+                ("frame_shift_ms", C.c_float), ("dither", C.c_float),
+                ("preemphasis_coefficient", C.c_float), ("remove_dc_offset", C.c_int),
+                ("num_mel_bins", C.c_int), ("low_freq", C.c_float), ("high_freq", C.c_float),
+                ("seed", C.c_uint64)]
+
+
+_FO = C.POINTER(FbankOpts)
 _SIGS = [
     ("vox_load", C.c_int, [C.c_char_p, C.c_int, C.c_int, C.POINTER(_P)]),
     ("vox_load_blob", C.c_int, [C.c_void_p, C.c_size_t, C.c_int, C.c_int, C.POINTER(_P)]),
@@ -57,6 +69,12 @@ _SIGS = [
                                       C.POINTER(C.c_size_t)]),
     ("vox_parse_mat_shape", C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(C.c_int),
                                       C.POINTER(C.c_int)]),
+    ("vox_fbank_default_opts", None, [_FO]),
+    ("vox_fbank_num_frames", C.c_int64, [C.c_int64, _FO]),
+    ("vox_fbank_device", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int64, _FO,
+                                   C.c_void_p, C.c_void_p]),
+    ("vox_sliding_cmn_device", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int,
+                                         C.c_int, C.c_void_p, C.c_void_p]),
     ("vox_format_vec_flt", C.c_int64, [C.c_char_p, _F, C.c_int, C.c_void_p, C.c_size_t,
                                        C.POINTER(C.c_int64)]),
 ]

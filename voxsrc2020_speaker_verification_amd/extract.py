@@ -25,10 +25,11 @@ import numpy as np
 from .extractor import MIN_FRAMES, chunk_plan
 
 
-def embed_utterances(feats, embed_batch, dim, batch=64):
+def embed_utterances(feats, embed_batch, dim, batch=64, stack=np.stack):
     """feats: list of (key, [T,F] float32).  embed_batch(x[n,L,F]) -> [n,dim].
     Returns [len(feats), dim] float32 in input order, applying the chunk rule
-    with chunks of equal length batched together."""
+    with chunks of equal length batched together.  `stack` builds a batch
+    from the chunk slices (torch.stack for device-resident features)."""
     plans = []
     buckets = {}
     for u, (key, f) in enumerate(feats):
@@ -43,7 +44,7 @@ def embed_utterances(feats, embed_batch, dim, batch=64):
     for L, items in buckets.items():
         for b in range(0, len(items), batch):
             part = items[b:b + batch]
-            x = np.stack([feats[u][1][s:s + L] for (u, ci, s) in part])
+            x = stack([feats[u][1][s:s + L] for (u, ci, s) in part])
             e = embed_batch(x)
             for (u, ci, s), row in zip(part, e):
                 chunk_emb[(u, ci)] = row

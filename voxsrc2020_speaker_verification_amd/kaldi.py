@@ -142,6 +142,20 @@ def format_vec_flt(key, v):
     return buf.raw[:need], off.value
 
 
+def format_mat_flt(key, m):
+    """Bytes of one binary FM ark record ("key \\0BFM \\4<i32 rows>\\4<i32 cols>
+    <f32 data>", kaldi_io.write_mat's layout, kaldi_io.py:508-540) and the
+    offset of its '\\0B' (for the scp)."""
+    m = np.ascontiguousarray(m, dtype=np.float32)
+    if m.ndim != 2:
+        raise ValueError("expected a 2-D matrix")
+    k = key.encode("utf-8")
+    if not k or b" " in k:
+        raise ValueError("key must be non-empty without spaces")
+    head = k + b" \0BFM \4" + np.int32(m.shape[0]).tobytes() + b"\4" + np.int32(m.shape[1]).tobytes()
+    return head + m.tobytes(), len(k) + 1
+
+
 class VectorWriter:
     """`ark,scp:<base>.ark,<base>.scp` writer of float vectors (copy-vector)."""
 
