@@ -35,7 +35,7 @@ def _kernel_name(tag, dt):
     if tag & (1 << 30):
         return "gemm1x1_wide"
     if tag & (1 << 29):
-        return "conv3x3_pipe"
+        return "conv3x3_win" if tag & (1 << 19) else "conv3x3_pipe"
     if tag & (1 << 28):
         return "gconv3x3_rows"
     if tag & (1 << 27):

@@ -230,6 +230,10 @@ struct vox_model {
   bool no_gemm_pipe = false;   // VOXEMB_NO_GEMM_PIPE=1: gemm1x1_lds instead of gemm1x1_pipe
   bool no_gemm_wide = false;   // VOXEMB_NO_GEMM_WIDE=1: gemm1x1_pipe instead of gemm1x1_wide
   bool no_s2_fused = false;    // VOXEMB_NO_S2_FUSED=1: 1x1a + split_s2_rows instead of s2_fused
+  // VOXEMB_CONV3_WIN=1: window-staged conv3x3_win for the w=96 stride-1 branches
+  // (bitwise equal; measured 115 us vs conv3x3_pipe's 97 us per L3 launch at
+  // B=256 -- twice the K-steps, each paying the ring's fixed per-step cost)
+  bool no_conv3_win = true;
   bool no_gconv = false;       // VOXEMB_NO_GCONV=1: grouped 3x3 on the generic implicit GEMM
   bool no_conv3 = false;
   bool no_gemm_pro = false;    // VOXEMB_NO_GEMM_PRO=1: prologue 1x1 convs off the pipelined GEMM       // VOXEMB_NO_CONV3=1: Res2Net w>=96 3x3 branches on conv_win/igemm
@@ -1138,6 +1142,8 @@ static int build_res2net(Builder& B, const float* x, int n, int t, float* out) {
           p.kh = br.kh; p.kw = br.kw; p.sh = p.sw = stride; p.dh = p.dw = 1; p.ph = p.pw = 1;
           p.groups = br.groups; p.flags = EPI_AFFINE | EPI_RELU;
           ok = br.wtc && br.mean && br.cin == w && br.cout == w && conv3_pipe_ok(p);
+          // stride-1 w = 96: input window staged once per tile (conv3w.hip)
+          if (ok && !m->no_conv3_win && conv3_win_ok(p)) op.type = 23;
           op.flops = 2.0 * n * Ho * Wo * 9.0 * br.cin * br.cout;
           op.bytes = (double)es * ((double)n * H * W * br.cin +
                                    (double)n * Ho * Wo * br.cout * (z ? 3.0 : 1.0));
@@ -1337,6 +1343,7 @@ static hipError_t run_op(vox_model* m, const Op& op, hipStream_t s) {
     case 13: return launch_chain_rows(op.ch, s);
     case 14: return launch_split_s2(op.ch, s);
     case 22: return launch_s2_fused(op.ch, s);
+    case 23: return launch_conv3_win(op.cp, m->num_cu, s);
     case 15: return launch_convert_bf16(op.src, (float*)op.dst, op.count, s);
     case 16: return launch_att_bias_tanh((float*)op.dst, (const float*)op.src, op.N, op.H, op.W, op.C, s);
     case 17:
@@ -1421,6 +1428,7 @@ extern "C" int vox_load_blob(const void* blob, size_t nbytes, int device, int pr
   if (const char* e = std::getenv("VOXEMB_NO_CHAIN_ROWS")) m->no_chain_rows = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_NO_SPLIT_S2")) m->no_split_s2 = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_NO_S2_FUSED")) m->no_s2_fused = std::atoi(e) != 0;
+  if (const char* e = std::getenv("VOXEMB_CONV3_WIN")) m->no_conv3_win = std::atoi(e) == 0;
   if (const char* e = std::getenv("VOXEMB_BNECK_NSEG")) m->bneck_nseg = std::atoi(e);
   if (const char* e = std::getenv("VOXEMB_BNECK_DBG")) m->bneck_dbg = std::atoi(e);
   if (const char* e = std::getenv("VOXEMB_CHAIN_R")) m->chain_r = std::atoi(e);
@@ -1593,6 +1601,8 @@ extern "C" int vox_profile(vox_model* m, const float* d_x, int n, int t, int f, 
         tag |= (1 << 30);
       else if (o.type == 22)
         tag |= (1 << 26) | (1 << 19);
+      else if (o.type == 23)
+        tag |= (1 << 29) | (1 << 19);
       else if (o.type == 8)
         tag |= (o.cl.wco << 4) | (o.cl.wpx << 8) | (((o.cp.cinp + 31) / 32) << 16) | (1 << 20);
       else if (o.type == 0 || o.type == 5)
@@ -1616,12 +1626,12 @@ extern "C" int vox_plan_describe(vox_model* m, const float* d_x, int n, int t, i
   static const char* tn[] = {"igemm", "reduce", "pool", "avgpool", "convert", "igemm32", "bnrelu",
                              "win", "rr", "gemm", "chain", "stem", "bneck", "chainrows", "splits2",
                              "cvt16", "atttanh", "attpool", "gemmpipe", "gconv", "conv3pipe",
-                             "gemmwide", "s2fused"};
+                             "gemmwide", "s2fused", "conv3win"};
   for (const Op& o : m->plan) {
     char line[256];
     const ConvParams& p = o.cp;
     if (o.type == 0 || o.type == 5 || o.type == 7 || o.type == 8 || o.type == 9 || o.type == 18 ||
-        o.type == 20 || o.type == 21)
+        o.type == 20 || o.type == 21 || o.type == 23)
       std::snprintf(line, sizeof(line),
                     "%s wco=%d wpx=%d s=%d N=%d H=%d W=%d Cin=%d Ho=%d Wo=%d Cout=%d k=%dx%d st=%d "
                     "g=%d flags=%d x2=%d pro=%d flops=%.4g bytes=%.4g\n",

@@ -116,6 +116,10 @@ hipError_t launch_gemm1x1(const ConvParams& p, hipStream_t s);
 // one workgroup per CU.  gemm_pipe_ok: K % 64 == 0, K >= 192, coutp % 128 == 0.
 int gemm_pipe_ok(const ConvParams& p);
 hipError_t launch_gemm_pipe(const ConvParams& p, int num_cu, int variant, hipStream_t s);
+// Window-staged 3x3 (conv3w.hip) for the w = 96 stride-1 branches at image
+// width 20 or 10: same tiles / epilogue / bits as conv3x3_pipe.
+int conv3_win_ok(const ConvParams& p);
+hipError_t launch_conv3_win(const ConvParams& p, int num_cu, hipStream_t s);
 // Wide-tile variant (gemm_wide.hip): 256 x BN tiles, BN = 256 (Cout % 256 == 0)
 // or 192 (Cout % 192 == 0, no residual), K % 32 == 0, K >= 96, no prologue.
 // gemm_wide_bn returns BN or 0 when it does not apply.
