@@ -21,7 +21,11 @@ __device__ __forceinline__ void wait_vm(int n) {
     W_(36) W_(40) W_(48) W_(56) default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 }
 
-__global__ __launch_bounds__(512) void probe(const char* buf, size_t span, int S, int D, int P, int nwaves_issue) {
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(512) void probe(const char* buf, size_t span, int S, int D, int P, int nwaves_issue,
+                                             int nmfma, float* sink, int mfma_wave_lo, int stagger) {
   extern __shared__ char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint32_t lds0 = (uint32_t)(uintptr_t)smem;
@@ -40,12 +44,25 @@ __global__ __launch_bounds__(512) void probe(const char* buf, size_t span, int S
     off = (off + slot_bytes) & mask;
   };
   for (int s = 0; s < D - 1; ++s) issue(s);
+  bf16x8 a = {}, b = {};
+  for (int e = 0; e < 8; ++e) { a[e] = (__bf16)(lane * 0.01f + e); b[e] = (__bf16)(wave * 0.1f - e); }
+  f32x4 acc[8] = {};
   for (int s = 0; s < S; ++s) {
     if (iss) wait_vm((D - 2) * P);
     __builtin_amdgcn_s_barrier();
-    issue(s + D - 1);
+    const bool late = stagger && wave >= 4;   // waves 4-7: MFMAs first, then their DMA
+    if (!late) issue(s + D - 1);
+    // nmfma independent 16x16x32 MFMAs per wave (8 accumulators round robin)
+    for (int m = 0; m < (wave >= mfma_wave_lo ? nmfma : 0); m += 8) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[k], 0, 0, 0);
+    }
+    if (late) issue(s + D - 1);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  float t = 0.f;
+  for (int k = 0; k < 8; ++k) t += acc[k][0] + acc[k][1] + acc[k][2] + acc[k][3];
+  if (t == 12345.f) sink[threadIdx.x] = t;   // keep the MFMAs alive
 }
 
 int main(int argc, char** argv) {
@@ -60,27 +77,29 @@ int main(int argc, char** argv) {
   hipEventCreate(&e1);
   printf("{\"cus\": %d, \"runs\": [\n", ncu);
   bool first = true;
+  float* sink;
+  hipMalloc(&sink, 4096);
+  struct Cfg { int nw, P, nm, lo, st; const char* name; };
+  const Cfg cfgs[] = {
+      {8, 4, 32, 0, 0, "all8: dma4+mfma32"}, {8, 4, 32, 0, 1, "all8 staggered: dma4+mfma32"},
+      {8, 4, 0, 0, 0, "all8: dma4 only"}, {8, 0, 32, 0, 0, "all8: mfma32 only"},
+      {4, 8, 64, 4, 0, "split: w0-3 dma8, w4-7 mfma64"},
+      {8, 2, 32, 0, 0, "all8: dma2+mfma32"}, {8, 2, 32, 0, 1, "all8 staggered: dma2+mfma32"},
+      {8, 4, 64, 0, 0, "all8: dma4+mfma64"}, {8, 4, 64, 0, 1, "all8 staggered: dma4+mfma64"}};
   for (size_t span : {(size_t)4 << 30, (size_t)64 << 20, (size_t)2 << 20}) {
-    for (int nw : {8, 4}) {
-      for (int P : {1, 2, 4, 8}) {
-        for (int D : {2, 3, 4}) {
-          const size_t lds = (size_t)D * nw * P * 1024;
-          if (lds > 160 * 1024 || (D - 2) * P > 56) continue;
-          const int S = 400;
-          hipLaunchKernelGGL(probe, dim3(ncu), dim3(512), lds, 0, buf, span, 50, D, P, nw);
-          hipEventRecord(e0);
-          hipLaunchKernelGGL(probe, dim3(ncu), dim3(512), lds, 0, buf, span, S, D, P, nw);
-          hipEventRecord(e1);
-          hipEventSynchronize(e1);
-          float ms;
-          hipEventElapsedTime(&ms, e0, e1);
-          const double per_step_ns = ms * 1e6 / S;
-          const double gbs_cu = (double)nw * P * 1024 / per_step_ns;
-          printf("%s{\"span_mb\": %zu, \"waves\": %d, \"P\": %d, \"D\": %d, \"inflight_kb\": %d, \"ns_step\": %.1f, \"gbs_cu\": %.1f, \"tbs_chip\": %.2f}",
-                 first ? "" : ",\n", span >> 20, nw, P, D, (D - 1) * nw * P, per_step_ns, gbs_cu, gbs_cu * ncu / 1000);
-          first = false;
-        }
-      }
+    for (const Cfg& c : cfgs) {
+      const int D = 4;
+      const size_t lds = (size_t)D * (c.nw ? c.nw : 1) * (c.P ? c.P : 1) * 1024;
+      const int S = 400;
+      hipLaunchKernelGGL(probe, dim3(ncu), dim3(512), lds, 0, buf, span, 50, D, c.P, c.P ? c.nw : 0, c.nm, sink, c.lo, c.st);
+      hipEventRecord(e0);
+      hipLaunchKernelGGL(probe, dim3(ncu), dim3(512), lds, 0, buf, span, S, D, c.P, c.P ? c.nw : 0, c.nm, sink, c.lo, c.st);
+      hipEventRecord(e1);
+      hipEventSynchronize(e1);
+      float ms;
+      hipEventElapsedTime(&ms, e0, e1);
+      printf("%s{\"span_mb\": %zu, \"cfg\": \"%s\", \"ns_step\": %.1f}", first ? "" : ",\n", span >> 20, c.name, ms * 1e6 / S);
+      first = false;
     }
   }
   printf("\n]}\n");
