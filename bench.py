@@ -43,7 +43,7 @@ def _kernel_name(tag, dt):
     if tag & (1 << 26):
         return "s2_fused" if tag & (1 << 19) else "split_s2_rows"
     if tag & (1 << 25):
-        return "chain_rows"
+        return "chain_fused" if tag & (1 << 19) else "chain_rows"
     if tag & (1 << 24):
         return "bneck_fused"
     if tag & (1 << 23):

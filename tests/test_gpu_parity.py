@@ -201,10 +201,11 @@ def test_extract_cli_end_to_end(weights, tmp_path):
 
 @pytest.mark.parametrize("unfused_env", [("VOXEMB_NO_BNECK",), ("VOXEMB_NO_CHAIN_ROWS",),
                                          ("VOXEMB_NO_SPLIT_S2",), ("VOXEMB_NO_GEMM_PIPE",),
-                                         ("VOXEMB_NO_S2_FUSED",),
+                                         ("VOXEMB_NO_S2_FUSED",), ("VOXEMB_NO_CHAIN_FUSED",),
                                          ("VOXEMB_NO_BNECK", "VOXEMB_NO_CHAIN", "VOXEMB_NO_SPLIT_S2",
                                           "VOXEMB_NO_GEMM_PIPE")],
-                         ids=["chain", "tiled_chain", "split_s2", "gemm_pipe", "s2_fused", "unfused"])
+                         ids=["chain", "tiled_chain", "split_s2", "gemm_pipe", "s2_fused", "chain_fused",
+                              "unfused"])
 @pytest.mark.parametrize("name,F,T,N", [("res2net50_w24_s4_c32", 80, 200, 3),
                                         ("res2net50_w24_s4_c32", 80, 37, 3),
                                         ("res2net50_w24_s4_c32", 40, 75, 2),
@@ -361,6 +362,33 @@ def test_s2_fused_bitwise(weights, F, T, N, monkeypatch):
     with _extractor(blob, "bf16") as ex:
         ref = ex.run(x)
         assert not any(l.startswith("s2fused") for l in ex.describe(torch.from_numpy(x).cuda()))
+    assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("name,F,T,N", [("res2net50_w24_s4_c32", 80, 200, 3),
+                                        ("res2net50_w24_s4_c32", 80, 200, 16),
+                                        ("res2net50_w24_s4_c32", 80, 37, 2),
+                                        ("res2net50_w24_s4_c32", 40, 75, 2),
+                                        ("res2net50_w24_s4_c32", 80, 27, 1),
+                                        ("res2net101_w24_s4_c32_att", 80, 64, 3)])
+def test_chain_fused_bitwise(weights, name, F, T, N, monkeypatch):
+    """The fused identity-block front half (1x1a on the staged input row, x_s
+    to the concat buffer, chain_rows' stages on the rows it leaves in LDS; odd
+    and tiny heights, row segments with recomputed warm-up rows) gives the same
+    bits as the 1x1a GEMM + chain_rows."""
+    import torch
+    from voxsrc2020_speaker_verification_amd import synth
+    spec, t, blob = weights(name, F)
+    x = synth.make_features(N, T, F, seed=37)
+    with _extractor(blob, "bf16") as ex:
+        got = ex.run(x)
+        assert any(l.startswith("chainfused") for l in ex.describe(torch.from_numpy(x).cuda()))
+    monkeypatch.setenv("VOXEMB_NO_CHAIN_FUSED", "1")
+    with _extractor(blob, "bf16") as ex:
+        ref = ex.run(x)
+        desc = ex.describe(torch.from_numpy(x).cuda())
+        assert not any(l.startswith("chainfused") for l in desc)
+        assert any(l.startswith("chainrows") for l in desc)
     assert np.array_equal(got, ref)
 
 

@@ -230,6 +230,7 @@ struct vox_model {
   bool no_gemm_pipe = false;   // VOXEMB_NO_GEMM_PIPE=1: gemm1x1_lds instead of gemm1x1_pipe
   bool no_gemm_wide = false;   // VOXEMB_NO_GEMM_WIDE=1: gemm1x1_pipe instead of gemm1x1_wide
   bool no_s2_fused = false;    // VOXEMB_NO_S2_FUSED=1: 1x1a + split_s2_rows instead of s2_fused
+  bool no_chain_fused = false; // VOXEMB_NO_CHAIN_FUSED=1: 1x1a + chain_rows instead of chain_fused
   // VOXEMB_CONV3_WIN=1: window-staged conv3x3_win for the w=96 stride-1 branches
   // (bitwise equal; measured 115 us vs conv3x3_pipe's 97 us per L3 launch at
   // B=256 -- twice the K-steps, each paying the ring's fixed per-step cost)
@@ -988,6 +989,42 @@ static int build_res2net(Builder& B, const float* x, int n, int t, float* out) {
           chained = pooled = true;
         }
       }
+      if (stride == 1 && m->dt == BF16 && !m->no_chain && !m->no_chain_rows &&
+          !m->no_chain_fused && cur.ld == cur.C && chain_fused_lds(cur.C, w, s, W) > 0) {
+        // 1x1a + row-streamed chain in one launch (bneck.hip chain_fused): only
+        // x_s of the 1x1a output reaches HBM
+        const ConvW& c1a = m->convs[ci];
+        bool ok = s - 1 <= 8 && c1a.wpair && c1a.mean && c1a.cin == cur.C && c1a.cout == sw;
+        for (int j = 0; ok && j < s - 1; ++j)
+          ok = m->convs[ci + 1 + j].wtc && m->convs[ci + 1 + j].coutp >= 16 * ((w + 15) / 16);
+        if (ok) {
+          ChainParams q{};
+          q.x = cur.p; q.ldx = cur.ld; q.cin = cur.C;
+          q.wa = c1a.wpair->p; q.ma = (const float*)c1a.mean->p; q.ia = (const float*)c1a.inv->p;
+          q.b = Bc; q.ldb = sw;
+          q.N = n; q.H = H; q.W = W; q.w = w; q.nst = s - 1;
+          int nseg = 1;
+          while (n * nseg < 256 && H / (2 * nseg) >= 16) nseg *= 2;
+          q.R = (H + nseg - 1) / nseg;
+          q.nwaves = (H + q.R - 1) / q.R;
+          for (int j = 0; j < s - 1; ++j) {
+            const ConvW& br = m->convs[ci + 1 + j];
+            q.wt[j] = br.wtc->p;
+            q.mean[j] = (const float*)br.mean->p;
+            q.inv[j] = (const float*)br.inv->p;
+          }
+          q.lds = chain_fused_lds(cur.C, w, s, W);
+          Op op;
+          op.kind = OP_CONV;
+          op.type = 24;
+          op.ch = q;
+          op.flops = 2.0 * n * H * W * ((double)cur.C * sw + 9.0 * w * w * (s - 1));
+          op.bytes = (double)es * n * H * W * ((double)cur.C + sw);
+          B.ops->push_back(op);
+          ci += s;
+          chained = true;
+        }
+      }
       const ConvW& c1a = m->convs[chained ? 0 : ci++];
       char* A = chained ? nullptr : B.base(S_A, (size_t)n * H * W * sw * es);
       if (chained) {
@@ -999,7 +1036,7 @@ static int build_res2net(Builder& B, const float* x, int n, int t, float* out) {
       } else {
         emit_conv(B, c1a, cur, nullptr, 0, 1, 1, 1, 1, 0, 0, H, W, A, sw, EPI_AFFINE | EPI_RELU);
       }
-      if (stride == 1 && m->dt == BF16 && !m->no_chain && !m->no_chain_rows &&
+      if (!chained && stride == 1 && m->dt == BF16 && !m->no_chain && !m->no_chain_rows &&
           chain_rows_lds(w, s, W) > 0) {
         // row-streamed chain (bneck.hip): no halo recompute
         bool ok = s - 1 <= 8;
@@ -1343,6 +1380,7 @@ static hipError_t run_op(vox_model* m, const Op& op, hipStream_t s) {
     case 13: return launch_chain_rows(op.ch, s);
     case 14: return launch_split_s2(op.ch, s);
     case 22: return launch_s2_fused(op.ch, s);
+    case 24: return launch_chain_fused(op.ch, s);
     case 23: return launch_conv3_win(op.cp, m->num_cu, s);
     case 15: return launch_convert_bf16(op.src, (float*)op.dst, op.count, s);
     case 16: return launch_att_bias_tanh((float*)op.dst, (const float*)op.src, op.N, op.H, op.W, op.C, s);
@@ -1428,6 +1466,7 @@ extern "C" int vox_load_blob(const void* blob, size_t nbytes, int device, int pr
   if (const char* e = std::getenv("VOXEMB_NO_CHAIN_ROWS")) m->no_chain_rows = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_NO_SPLIT_S2")) m->no_split_s2 = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_NO_S2_FUSED")) m->no_s2_fused = std::atoi(e) != 0;
+  if (const char* e = std::getenv("VOXEMB_NO_CHAIN_FUSED")) m->no_chain_fused = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_CONV3_WIN")) m->no_conv3_win = std::atoi(e) == 0;
   if (const char* e = std::getenv("VOXEMB_BNECK_NSEG")) m->bneck_nseg = std::atoi(e);
   if (const char* e = std::getenv("VOXEMB_BNECK_DBG")) m->bneck_dbg = std::atoi(e);
@@ -1603,6 +1642,8 @@ extern "C" int vox_profile(vox_model* m, const float* d_x, int n, int t, int f, 
         tag |= (1 << 26) | (1 << 19);
       else if (o.type == 23)
         tag |= (1 << 29) | (1 << 19);
+      else if (o.type == 24)
+        tag |= (1 << 25) | (1 << 19);
       else if (o.type == 8)
         tag |= (o.cl.wco << 4) | (o.cl.wpx << 8) | (((o.cp.cinp + 31) / 32) << 16) | (1 << 20);
       else if (o.type == 0 || o.type == 5)
@@ -1626,7 +1667,7 @@ extern "C" int vox_plan_describe(vox_model* m, const float* d_x, int n, int t, i
   static const char* tn[] = {"igemm", "reduce", "pool", "avgpool", "convert", "igemm32", "bnrelu",
                              "win", "rr", "gemm", "chain", "stem", "bneck", "chainrows", "splits2",
                              "cvt16", "atttanh", "attpool", "gemmpipe", "gconv", "conv3pipe",
-                             "gemmwide", "s2fused", "conv3win"};
+                             "gemmwide", "s2fused", "conv3win", "chainfused"};
   for (const Op& o : m->plan) {
     char line[256];
     const ConvParams& p = o.cp;
@@ -1646,10 +1687,10 @@ extern "C" int vox_plan_describe(vox_model* m, const float* d_x, int n, int t, i
       std::snprintf(line, sizeof(line), "gconv N=%d H=%d W=%d C=%d gw=%d Ho=%d Wo=%d st=%d rs=%d seg=%d nseg=%d flops=%.4g bytes=%.4g\n",
                     o.gq.N, o.gq.H, o.gq.W, o.gq.C, o.gq.gw, o.gq.Ho, o.gq.Wo, o.gq.sh,
                     gconv_rs(o.gq), o.gq.seg, o.gq.nseg, o.flops, o.bytes);
-    else if (o.type == 22)
-      std::snprintf(line, sizeof(line), "s2fused N=%d H=%d W=%d Cin=%d w=%d nst=%d seg=%d nseg=%d lds=%d flops=%.4g bytes=%.4g\n",
-                    o.ch.N, o.ch.H, o.ch.W, o.ch.cin, o.ch.w, o.ch.nst, o.ch.R, o.ch.nwaves, o.ch.lds,
-                    o.flops, o.bytes);
+    else if (o.type == 22 || o.type == 24)
+      std::snprintf(line, sizeof(line), "%s N=%d H=%d W=%d Cin=%d w=%d nst=%d seg=%d nseg=%d lds=%d flops=%.4g bytes=%.4g\n",
+                    tn[o.type], o.ch.N, o.ch.H, o.ch.W, o.ch.cin, o.ch.w, o.ch.nst, o.ch.R,
+                    o.ch.nwaves, o.ch.lds, o.flops, o.bytes);
     else if (o.type == 14)
       std::snprintf(line, sizeof(line), "splits2 N=%d H=%d W=%d w=%d nst=%d seg=%d nseg=%d lds=%d flops=%.4g bytes=%.4g\n",
                     o.ch.N, o.ch.H, o.ch.W, o.ch.w, o.ch.nst, o.ch.R, o.ch.nwaves, o.ch.lds,

@@ -637,6 +637,295 @@ __global__ __launch_bounds__((ChainRowsCfg<WID, S, PT>::NT)) void chain_rows(Cha
   }
 }
 
+// ----------------------------------------------------------------------------
+// Identity-block front half in one launch (res2net_model.py:90-93 + 53-75,
+// layer 2 blocks 1..): the 1x1a (+BN+ReLU, K = Cin) on the block input and
+// chain_rows' row-streamed split chain, so the 1x1a output never touches HBM
+// (only x_S, which the 1x1c reads, is written there).  Step for A-row a:
+//   phase A: wave t computes 16 1x1a channels of row a from the staged input
+//            row (weights in registers) -> rings x_1 (= z_1), x_2 .. x_{S-1};
+//            x_S -> the concat buffer (global);
+//   phase B: chain_rows' stage waves, stage k on row a-2k+1.
+// The next input row streams global -> registers during the step and lands in
+// the staging buffer at its end.  Same roundings and K orders as the unfused
+// 1x1a + chain_rows: bit-identical.
+template <int CI, int WID, int S, int PT>
+struct ChainFusedCfg {
+  using R = ChainRowsCfg<WID, S, PT>;
+  static constexpr int SW = S * WID;
+  static constexpr int NW = SW / 16;                   // one 1x1a 16-channel tile per wave
+  static constexpr int NT = 64 * NW;
+  static constexpr int KSA = CI / 32;
+  static constexpr int IU = ((CI / 8) & 1) ? CI / 8 : CI / 8 + 1;
+  static constexpr int ISTR = IU * 16;                 // staged input pixel stride
+  static constexpr int INB = 16 * PT * ISTR;
+  static constexpr int CU = CI / 8;
+  static constexpr int XREG = (16 * PT * CU + NT - 1) / NT;
+  static constexpr int LDS = R::RING_BYTES + INB + 4 * (2 * (S - 1) * 16 * R::WCO + 2 * SW);
+  static_assert(NW >= R::ROLES, "every chain role needs a wave");
+};
+
+template <int CI, int WID, int S, int PT>
+__global__ __launch_bounds__((ChainFusedCfg<CI, WID, S, PT>::NT)) void chain_fused(ChainParams q) {
+  using K = ChainFusedCfg<CI, WID, S, PT>;
+  using R = typename K::R;
+  constexpr int NT = K::NT, WCO = R::WCO, KST = R::KST, ASTR = R::ASTR, ROWB = R::ROWB;
+  static_assert(CI % 32 == 0 && WID % 8 == 0 && K::SW % 32 == 0, "shape");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int col = lane & 15, g = lane >> 4;
+  const int H = q.H, W = q.W;
+  const int nseg = q.nwaves;
+  const int n = blockIdx.x / nseg;
+  const int h0 = (blockIdx.x - n * nseg) * q.R;
+  const int h1 = min(H, h0 + q.R);
+  char* rings = smem;
+  char* inb = smem + R::RING_BYTES;
+  float* bmb = reinterpret_cast<float*>(inb + K::INB);
+  float* bib = bmb + (S - 1) * 16 * WCO;
+  float* bma = bib + (S - 1) * 16 * WCO;
+  float* bia = bma + K::SW;
+  const bf16_t* __restrict__ X = reinterpret_cast<const bf16_t*>(q.x);
+  bf16_t* __restrict__ Bo = reinterpret_cast<bf16_t*>(q.b);
+  const size_t img = (size_t)n * H * W;
+
+  for (int i = tid; i < R::RING_BYTES / 16; i += NT)
+    reinterpret_cast<uint4*>(rings)[i] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+  for (int k = 0; k < S - 1; ++k)
+    for (int c = tid; c < 16 * WCO; c += NT) {
+      bmb[k * 16 * WCO + c] = c < WID ? q.mean[k][c] : 0.f;
+      bib[k * 16 * WCO + c] = c < WID ? q.inv[k][c] : 0.f;
+    }
+  for (int c = tid; c < K::SW; c += NT) {
+    bma[c] = q.ma[c];
+    bia[c] = q.ia[c];
+  }
+
+  const bool role = wave < R::ROLES;
+  const int ck = role ? wave / WCO + 1 : 1;
+  const int ci = wave % WCO;
+  bf16x8 wb[KST];
+  {
+    const void* wk = q.wt[0];
+#pragma unroll
+    for (int k = 1; k < S - 1; ++k)
+      if (ck == k + 1) wk = q.wt[k];
+    const bf16_t* __restrict__ Wk = reinterpret_cast<const bf16_t*>(wk);
+#pragma unroll
+    for (int s = 0; s < KST; ++s) {
+      const int kk = 32 * s + 8 * g;
+      wb[s] = (role && kk < R::KFLAT) ? ld16(Wk + (size_t)(ci * 16 + col) * R::KFLAT + kk)
+                                      : bf16x8{};
+    }
+  }
+  // 1x1a tile t of the paired-row weights: lane channels 32(t/2) + 8g + 4(t%2) + 0..3
+  const int t16 = wave;
+  bf16x8 w1[K::KSA];
+  {
+    const bf16_t* __restrict__ Wa = reinterpret_cast<const bf16_t*>(q.wa);
+#pragma unroll
+    for (int s = 0; s < K::KSA; ++s)
+      w1[s] = ld16(Wa + (size_t)(t16 * 16 + col) * CI + 32 * s + 8 * g);
+  }
+
+  // input rows: global -> registers (one step ahead) -> staging
+  uint4 xr[K::XREG];
+  const int ldx = q.ldx;
+  auto load_x = [&](int r) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < K::XREG; ++i) {
+      int c = tid + i * NT;
+      asm volatile("" : "+v"(c));   // recomputed per step: nothing hoisted into registers
+      const int px = c / K::CU, u = c - px * K::CU;
+      xr[i] = make_uint4(0, 0, 0, 0);
+      if (c < 16 * PT * K::CU && px < W && r >= 0 && r < H)
+        xr[i] = *reinterpret_cast<const uint4*>(X + (img + (size_t)r * W + px) * ldx + u * 8);
+    }
+  };
+  auto store_x = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < K::XREG; ++i) {
+      int c = tid + i * NT;
+      asm volatile("" : "+v"(c));
+      const int px = c / K::CU, u = c - px * K::CU;
+      if (c < 16 * PT * K::CU) *reinterpret_cast<uint4*>(inb + px * K::ISTR + u * 16) = xr[i];
+    }
+  };
+
+  const int a0 = h0 - (S - 1);
+  const int steps = (h1 - h0) + 3 * (S - 1) - 1;   // as chain_rows
+  load_x(a0);
+  store_x();
+  __syncthreads();
+  for (int t = 0; t < steps; ++t) {
+    const int a = a0 + t;
+    load_x(a + 1);   // lands during phase A, goes to the staging after it
+    // ---------------- phase A: 1x1a of A-row a -> rings / x_S
+    {
+      const int ch = 32 * (t16 >> 1) + 8 * g + 4 * (t16 & 1);
+      const int p = ch / WID, off = ch - p * WID;
+      const bool inimg = a >= 0 && a < H;
+      int sl = (a + 840) % 3;                                   // plane 0 -> z_1
+#pragma unroll
+      for (int d = 2; d < S; ++d)
+        if (p + 1 == d) sl = R::ZEND + (d - 2) * (d - 1) + (a + 840) % (2 * d - 2);
+      const bool last = p == S - 1;                             // x_S: global only
+      const bool emit_s = last && inimg && a >= h0 && a < h1;
+      char* dst = rings + sl * ROWB + off * 2;
+      const f32x4 m0 = *reinterpret_cast<const f32x4*>(bma + ch);
+      const f32x4 i0 = *reinterpret_cast<const f32x4*>(bia + ch);
+      const char* src = inb + (8 * g) * 2;
+      // the PT pixel tiles as independent accumulators, fragments read one
+      // k-step ahead (same K order per tile as the GEMM)
+      f32x4 acc[PT];
+      bf16x8 bc[PT], bn[PT];
+#pragma unroll
+      for (int j = 0; j < PT; ++j) {
+        acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const int px = 16 * j + col;
+        const int pr = px < W ? px : W - 1;
+        bc[j] = *reinterpret_cast<const bf16x8*>(src + pr * K::ISTR);
+      }
+#pragma unroll
+      for (int s = 0; s < K::KSA; ++s) {
+        if (s + 1 < K::KSA) {
+#pragma unroll
+          for (int j = 0; j < PT; ++j) {
+            const int px = 16 * j + col;
+            const int pr = px < W ? px : W - 1;
+            bn[j] = *reinterpret_cast<const bf16x8*>(src + pr * K::ISTR + 64 * (s + 1));
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < PT; ++j) acc[j] = mfma_step(w1[s], bc[j], acc[j]);
+#pragma unroll
+        for (int j = 0; j < PT; ++j) bc[j] = bn[j];
+        __builtin_amdgcn_sched_barrier(0);   // reads stay one k-step ahead
+      }
+#pragma unroll
+      for (int j = 0; j < PT; ++j) {
+        const int px = 16 * j + col;
+        bf16x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = (bf16_t)fmaxf((acc[j][e] - m0[e]) * i0[e], 0.f);
+        if (!inimg) o = bf16x4{};   // SAME padding rows of the chain
+        if (px < W) {
+          if (!last) *reinterpret_cast<bf16x4*>(dst + (px + 1) * ASTR) = o;
+          else if (emit_s)
+            *reinterpret_cast<bf16x4*>(Bo + (img + (size_t)a * W + px) * q.ldb + ch) = o;
+        }
+      }
+    }
+    __syncthreads();
+    store_x();   // input row a+1: phase A is done with the staging; xr dies here
+    // ---------------- phase B: chain_rows' stages, stage k on row a-2k+1
+    if (role) {
+      const int k = ck;
+      const int co = 16 * ci + 4 * g;
+      const int r = a - 2 * k + 1;
+      const bool inimg = r >= 0 && r < H;
+      const int zd = k == 1 ? 3 : 4;
+      const int zbase = k == 1 ? 0 : 3 + 4 * (k - 2);
+      // row offsets relative to the stage's z ring (< 64 KB: packed two per register)
+      const int rb0 = __builtin_amdgcn_readfirstlane(((r - 1 + 840) % zd) * ROWB);
+      const int rb1 = __builtin_amdgcn_readfirstlane(((r + 840) % zd) * ROWB);
+      const int rb2 = __builtin_amdgcn_readfirstlane(((r + 1 + 840) % zd) * ROWB);
+      const char* zring = rings + zbase * ROWB + col * ASTR;
+      const bool chain_next = k < S - 1;
+      const int zsl = __builtin_amdgcn_readfirstlane((3 + 4 * (k - 1) + (r + 840) % 4) * ROWB);
+      const int xsl = __builtin_amdgcn_readfirstlane(
+          (R::ZEND + (k - 1) * k + (r + 840) % (2 * k)) * ROWB);
+      const f32x4 m = *reinterpret_cast<const f32x4*>(bmb + (k - 1) * 16 * WCO + co);
+      const f32x4 sc = *reinterpret_cast<const f32x4*>(bib + (k - 1) * 16 * WCO + co);
+      const bool emit = r >= h0 && r < h1;
+      constexpr int KP = (KST + 1) / 2;
+      unsigned bpk[KP];
+#pragma unroll
+      for (int s = 0; s < KST; ++s) {   // per-step tap offsets (no table kept live)
+        int kk = 32 * s + 8 * g;
+        asm volatile("" : "+v"(kk));
+        int dyi = 1, off = 0;
+        if (kk < R::KFLAT) {
+          const int tap = kk / WID, ch = kk - tap * WID;
+          dyi = tap / 3;
+          off = (tap % 3 - 1) * ASTR + ch * 2;
+        }
+        const unsigned rel = (dyi == 0 ? rb0 : (dyi == 1 ? rb1 : rb2)) + off + ASTR;
+        if (s & 1) bpk[s >> 1] |= rel << 16;
+        else bpk[s >> 1] = rel;
+      }
+      auto boff = [&](int s) __attribute__((always_inline)) {
+        return (s & 1) ? (bpk[s >> 1] >> 16) : (bpk[s >> 1] & 0xFFFFu);
+      };
+      auto epilogue = [&](const f32x4& acc, int px) __attribute__((always_inline)) {
+        if (!(co < WID && px < W)) return;
+        const int pxo = px * ASTR + co * 2 + ASTR;
+        bf16x4 y;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) y[e] = (bf16_t)fmaxf((acc[e] - m[e]) * sc[e], 0.f);
+        if (emit)
+          *reinterpret_cast<bf16x4*>(Bo + (img + (size_t)r * W + px) * q.ldb + (k - 1) * WID + co) = y;
+        if (chain_next) {
+          const bf16x4 x = *reinterpret_cast<const bf16x4*>(rings + xsl + pxo);
+          *reinterpret_cast<bf16x4*>(rings + zsl + pxo) = inimg ? add4(x, y) : bf16x4{};
+        }
+      };
+      f32x4 acc[PT];
+      bf16x8 bc[PT], bn[PT];
+#pragma unroll
+      for (int j = 0; j < PT; ++j) {
+        acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        bc[j] = *reinterpret_cast<const bf16x8*>(zring + boff(0) + 16 * j * ASTR);
+      }
+#pragma unroll
+      for (int s = 0; s < KST; ++s) {
+        if (s + 1 < KST) {
+#pragma unroll
+          for (int j = 0; j < PT; ++j)
+            bn[j] = *reinterpret_cast<const bf16x8*>(zring + boff(s + 1) + 16 * j * ASTR);
+        }
+#pragma unroll
+        for (int j = 0; j < PT; ++j) acc[j] = mfma_step(wb[s], bc[j], acc[j]);
+#pragma unroll
+        for (int j = 0; j < PT; ++j) bc[j] = bn[j];
+        __builtin_amdgcn_sched_barrier(0);   // reads stay one k-step ahead
+      }
+#pragma unroll
+      for (int j = 0; j < PT; ++j) epilogue(acc[j], 16 * j + col);
+    }
+    __syncthreads();
+  }
+}
+
+#define CHAIN_FUSED_SHAPES(X) \
+  X(256, 48, 4, 3)  /* res2net50_w24_s4_c32 layer-2 identity blocks, 80-d features (W = 40) */ \
+  X(256, 48, 4, 2)  /* ... 40-d features (W = 20) */
+
+int chain_fused_lds(int ci, int wid, int s, int W) {
+  const int pt = (W + 15) / 16;
+#define X_LDS(ci_, w_, s_, p_) \
+  if (ci == ci_ && wid == w_ && s == s_ && pt == p_) return ChainFusedCfg<ci_, w_, s_, p_>::LDS;
+  CHAIN_FUSED_SHAPES(X_LDS)
+#undef X_LDS
+  return -1;
+}
+
+hipError_t launch_chain_fused(const ChainParams& q, hipStream_t st) {
+  const int pt = (q.W + 15) / 16;
+#define X_LAUNCH(ci_, w_, s_, p_)                                                          \
+  if (q.cin == ci_ && q.w == w_ && q.nst + 1 == s_ && pt == p_) {                         \
+    using K = ChainFusedCfg<ci_, w_, s_, p_>;                                             \
+    hipLaunchKernelGGL((chain_fused<ci_, w_, s_, p_>), dim3(q.N * q.nwaves), dim3(K::NT), \
+                       K::LDS, st, q);                                                    \
+    return hipGetLastError();                                                             \
+  }
+  CHAIN_FUSED_SHAPES(X_LAUNCH)
+#undef X_LAUNCH
+  return hipErrorInvalidValue;
+}
+
 #define CHAIN_ROWS_SHAPES(X) \
   X(48, 4, 3)  /* res2net50_w24_s4_c32 layer 2, 80-d features (W = 40) */ \
   X(48, 4, 2)  /* ... 40-d features (W = 20) */

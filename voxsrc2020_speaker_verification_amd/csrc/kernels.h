@@ -67,6 +67,11 @@ hipError_t launch_split_chain(const ChainParams& q, int wco, int wpx, hipStream_
 // segments per utterance (grid N * q.nwaves); LDS bytes or -1 if no instance.
 int chain_rows_lds(int w, int split, int W);
 hipError_t launch_chain_rows(const ChainParams& q, hipStream_t s);
+// Identity-block front half (bneck.hip): 1x1a + BN + ReLU of q.x (q.cin
+// channels, weights q.wa) feeding chain_rows' stages in the same launch; x_S
+// is written to q.b at channel (S-1)*w.  LDS bytes or -1.
+int chain_fused_lds(int cin, int wid, int split, int W);
+hipError_t launch_chain_fused(const ChainParams& q, hipStream_t s);
 // Stride-2 split (bneck.hip): branches k < split-1 (3x3 s2 + BN + ReLU) and the
 // last split's 3x3/2 average pool, q.R output rows per segment, q.nwaves
 // segments per utterance; q.H/q.W are the INPUT dims.  LDS bytes or -1.
