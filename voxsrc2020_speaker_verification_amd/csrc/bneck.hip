@@ -91,7 +91,8 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
   constexpr int NW = K::NW, NT = K::NT, WCO = K::WCO, KST = K::KST;
   constexpr int ASTR = K::ASTR, ROWB = K::ROWB;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: scalar ring math
   const int col = lane & 15, g = lane >> 4;
   const int H = q.H, W = q.W;
   const int n = blockIdx.x / q.nseg;
@@ -184,49 +185,58 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
   }
 
   // ---- input rows: global -> registers (prefetch) -> LDS
-  uint4 inr[K::IREG];
-  auto load_in = [&](int r) __attribute__((always_inline)) {
+  // two register sets each for the input rows and the residual rows: a row is
+  // requested two steps before it is used (HBM latency under load exceeds a step)
+  uint4 inr[2][K::IREG];
+  auto load_in = [&](auto P, int r) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < K::IREG; ++i) {
       const int c = tid + i * NT;
       const int px = c / K::CU, u = c - px * K::CU;
-      inr[i] = make_uint4(0, 0, 0, 0);
+      inr[P][i] = make_uint4(0, 0, 0, 0);
       if (c < 16 * PT * K::CU && px < W && r >= 0 && r < H)
-        inr[i] = *reinterpret_cast<const uint4*>(X + (img + (size_t)r * W + px) * CI + u * 8);
+        inr[P][i] = *reinterpret_cast<const uint4*>(X + (img + (size_t)r * W + px) * CI + u * 8);
     }
   };
-  auto store_in = [&]() __attribute__((always_inline)) {
+  auto store_in = [&](auto P) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < K::IREG; ++i) {
       const int c = tid + i * NT;
       const int px = c / K::CU, u = c - px * K::CU;
-      if (c < 16 * PT * K::CU) *reinterpret_cast<uint4*>(inb + px * K::ISTR + u * 16) = inr[i];
+      if (c < 16 * PT * K::CU) *reinterpret_cast<uint4*>(inb + px * K::ISTR + u * 16) = inr[P][i];
     }
   };
-  bf16x8 res[PT];
-  auto load_res = [&](int r) __attribute__((always_inline)) {
+  bf16x8 resb[2][PT];
+  auto load_res = [&](auto P, int r) __attribute__((always_inline)) {
 #pragma unroll
     for (int j = 0; j < PT; ++j) {
       const int px = 16 * j + col;
       // identity: this lane's 8 residual channels; projection: its B chunk of
       // the (CI = 32)-channel input row, for the shortcut MFMAs
       const int cho = K::PROJ ? 8 * g : 32 * pq + 8 * g;
-      res[j] = (is_c && r >= h0 && r < h1 && px < W)
+      resb[P][j] = (is_c && r >= h0 && r < h1 && px < W)
                    ? ld16(X + (img + (size_t)r * W + px) * CI + cho) : bf16x8{};
     }
   };
 
   const int a0 = h0 - (S - 1);
   const int steps = (h1 - h0) + 3 * (S - 1);
-  load_in(a0);
-  store_in();
-  load_res(a0 - K::LAG_C);
+  using P0 = std::integral_constant<int, 0>;
+  using P1 = std::integral_constant<int, 1>;
+  load_in(P0{}, a0);
+  store_in(P0{});
+  load_in(P0{}, a0 + 1);
+  load_in(P1{}, a0 + 2);
+  load_res(P0{}, a0 - K::LAG_C);
+  load_res(P1{}, a0 - K::LAG_C + 1);
   __syncthreads();
 
-  for (int t = 0; t < steps; ++t) {
+  // step t (register set P = t & 1): rows a + 1 (input) and c (residual) were
+  // requested two steps earlier
+  auto step = [&](auto P, int t) __attribute__((always_inline)) {
     const int a = a0 + t;
     const int c = a - K::LAG_C;
-    if (!(q.dbg & 8)) load_in(a + 1);  // lands during this step, goes to LDS in phase 1
+    auto& res = resb[P];
     // ---------------- phase 0: 1x1a (row a) | 1x1c (row c)
     if (is_a && !(q.dbg & 1)) {
       const bool inimg = a >= 0 && a < H;
@@ -345,10 +355,13 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
         if (two) epi(c0, c1, res[(j + 1) < PT ? j + 1 : j], px + 16);
       }
     }
-    if (!(q.dbg & 8)) load_res(c + 1);
+    if (!(q.dbg & 8)) load_res(P, c + 2);
     __syncthreads();
     // ---------------- phase 1: all 3x3 stages, stage k on row a-2k+1
-    if (!(q.dbg & 8)) store_in();
+    if (!(q.dbg & 8)) {
+      store_in(P);
+      load_in(P, a + 3);
+    }
     if (chain_wave && !(q.dbg & 4)) {
       const int k = ck;
       const int co = 16 * ci + 4 * g;
@@ -411,6 +424,10 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
       }
     }
     __syncthreads();
+  };
+  for (int t = 0; t < steps; t += 2) {
+    step(P0{}, t);
+    if (t + 1 < steps) step(P1{}, t + 1);
   }
 }
 
@@ -487,7 +504,8 @@ __global__ __launch_bounds__((ChainRowsCfg<WID, S, PT>::NT)) void chain_rows(Cha
   using K = ChainRowsCfg<WID, S, PT>;
   constexpr int NT = K::NT, WCO = K::WCO, KST = K::KST, ASTR = K::ASTR, ROWB = K::ROWB;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: scalar ring math
   const int col = lane & 15, g = lane >> 4;
   const int H = q.H, W = q.W;
   const int nseg = q.nwaves;                 // segments per utterance (reused field)
@@ -656,20 +674,47 @@ struct ChainFusedCfg {
   static constexpr int NW = SW / 16;                   // one 1x1a 16-channel tile per wave
   static constexpr int NT = 64 * NW;
   static constexpr int KSA = CI / 32;
-  static constexpr int IU = ((CI / 8) & 1) ? CI / 8 : CI / 8 + 1;
-  static constexpr int ISTR = IU * 16;                 // staged input pixel stride
-  static constexpr int INB = 16 * PT * ISTR;
+  // LDS images (16-B units): chunk c (8 channels) of pixel slot x sits in
+  // sub-plane c/2 at unit 2x + ((c & 1) ^ bit2(x)).  gfx950 serves a
+  // ds_read_b128 in lane groups that pair 8 columns of lane group g (even)
+  // with 8 of g+1, which read chunks c and c+1: the two halves land on
+  // opposite unit parities and 8 distinct pixel residues, so fragment reads
+  // are conflict-free (the odd pixel stride of chain_rows conflicts 2-way);
+  // the bit-2 flip halves the conflicts of the 8-byte epilogue stores.
+  static constexpr int WR = 16 * PT + 2;                // ring slots: pad | pixels | pad
+  static constexpr int NCH = WID / 8;
+  static constexpr int SPR = 2 * WR;                   // units per sub-plane
+  static constexpr int ROWB = NCH / 2 * SPR * 16;
+  // z_k rings (k = 1..S-1) 4 rows each, so that the tap rows of a stage wrap
+  // with a mask; x_k (k = 2..S-1) 2k-2 rows
+  static constexpr int ZEND = 4 * (S - 1);
+  static constexpr int NPLANES = ZEND + (S - 2) * (S - 1);
+  static constexpr int RING_BYTES = NPLANES * ROWB;
+  static constexpr int KST = R::KST;
+  static constexpr int KTB = 64 * ((KST + 1) / 2) * 4;    // tap table [lane][k-step] u16
   static constexpr int CU = CI / 8;
+  static constexpr int SPX = 2 * 16 * PT + 2;          // staging sub-plane (= 2 mod 8: store_x)
+  static constexpr int INB = CU / 2 * SPX * 16;
   static constexpr int XREG = (16 * PT * CU + NT - 1) / NT;
-  static constexpr int LDS = R::RING_BYTES + INB + 4 * (2 * (S - 1) * 16 * R::WCO + 2 * SW);
+  static constexpr int LDS = RING_BYTES + INB + KTB + 4 * (2 * (S - 1) * 16 * R::WCO + 2 * SW);
+  static_assert(4 * ROWB < 65536, "tap offsets in 16 bits");
   static_assert(NW >= R::ROLES, "every chain role needs a wave");
+  static_assert(NCH % 2 == 0 && CU % 2 == 0, "chunk pairs");
+  static_assert(SPX % 8 == 2, "staging stores");
 };
+
+// byte offset of (pixel slot x, channel ch) in a chain_fused ring row
+template <int SPR>
+__device__ __forceinline__ int cf_off(int x, int ch) {
+  const int c = ch >> 3;
+  return ((c >> 1) * SPR + 2 * x + ((c & 1) ^ ((x >> 2) & 1))) * 16 + (ch & 7) * 2;
+}
 
 template <int CI, int WID, int S, int PT>
 __global__ __launch_bounds__((ChainFusedCfg<CI, WID, S, PT>::NT)) void chain_fused(ChainParams q) {
   using K = ChainFusedCfg<CI, WID, S, PT>;
   using R = typename K::R;
-  constexpr int NT = K::NT, WCO = R::WCO, KST = R::KST, ASTR = R::ASTR, ROWB = R::ROWB;
+  constexpr int NT = K::NT, WCO = R::WCO, KST = R::KST, ROWB = K::ROWB, SPR = K::SPR;
   static_assert(CI % 32 == 0 && WID % 8 == 0 && K::SW % 32 == 0, "shape");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -681,8 +726,9 @@ __global__ __launch_bounds__((ChainFusedCfg<CI, WID, S, PT>::NT)) void chain_fus
   const int h0 = (blockIdx.x - n * nseg) * q.R;
   const int h1 = min(H, h0 + q.R);
   char* rings = smem;
-  char* inb = smem + R::RING_BYTES;
-  float* bmb = reinterpret_cast<float*>(inb + K::INB);
+  char* inb = smem + K::RING_BYTES;
+  unsigned short* ktl = reinterpret_cast<unsigned short*>(inb + K::INB);
+  float* bmb = reinterpret_cast<float*>(inb + K::INB + K::KTB);
   float* bib = bmb + (S - 1) * 16 * WCO;
   float* bma = bib + (S - 1) * 16 * WCO;
   float* bia = bma + K::SW;
@@ -690,7 +736,7 @@ __global__ __launch_bounds__((ChainFusedCfg<CI, WID, S, PT>::NT)) void chain_fus
   bf16_t* __restrict__ Bo = reinterpret_cast<bf16_t*>(q.b);
   const size_t img = (size_t)n * H * W;
 
-  for (int i = tid; i < R::RING_BYTES / 16; i += NT)
+  for (int i = tid; i < K::RING_BYTES / 16; i += NT)
     reinterpret_cast<uint4*>(rings)[i] = make_uint4(0, 0, 0, 0);
 #pragma unroll
   for (int k = 0; k < S - 1; ++k)
@@ -701,6 +747,20 @@ __global__ __launch_bounds__((ChainFusedCfg<CI, WID, S, PT>::NT)) void chain_fus
   for (int c = tid; c < K::SW; c += NT) {
     bma[c] = q.ma[c];
     bia[c] = q.ia[c];
+  }
+  // tap table: for lane l and k-step s, the byte offset of its B fragment in
+  // the 4-row z ring counted from the slot of tap row 0 (before wrapping)
+  for (int e = tid; e < 64 * KST; e += NT) {
+    const int l = e / KST, st = e - l * KST;
+    const int kk = 32 * st + 8 * (l >> 4);
+    int dyi = 1, dx = 0, ch = 0;
+    if (kk < R::KFLAT) {
+      const int tap = kk / WID;
+      ch = kk - tap * WID;
+      dyi = tap / 3;
+      dx = tap % 3 - 1;
+    }
+    ktl[l * ((KST + 1) / 2) * 2 + st] = (unsigned short)(dyi * ROWB + cf_off<SPR>((l & 15) + 1 + dx, ch));
   }
 
   const bool role = wave < R::ROLES;
@@ -750,7 +810,8 @@ __global__ __launch_bounds__((ChainFusedCfg<CI, WID, S, PT>::NT)) void chain_fus
       int c = tid + i * NT;
       asm volatile("" : "+v"(c));
       const int px = c / K::CU, u = c - px * K::CU;
-      if (c < 16 * PT * K::CU) *reinterpret_cast<uint4*>(inb + px * K::ISTR + u * 16) = xr[i];
+      if (c < 16 * PT * K::CU)
+        *reinterpret_cast<uint4*>(inb + ((u >> 1) * K::SPX + 2 * px + (u & 1)) * 16) = xr[i];
     }
   };
 
@@ -767,36 +828,40 @@ __global__ __launch_bounds__((ChainFusedCfg<CI, WID, S, PT>::NT)) void chain_fus
       const int ch = 32 * (t16 >> 1) + 8 * g + 4 * (t16 & 1);
       const int p = ch / WID, off = ch - p * WID;
       const bool inimg = a >= 0 && a < H;
-      int sl = (a + 840) % 3;                                   // plane 0 -> z_1
+      int sl = (a + 840) & 3;                                   // plane 0 -> z_1
 #pragma unroll
       for (int d = 2; d < S; ++d)
-        if (p + 1 == d) sl = R::ZEND + (d - 2) * (d - 1) + (a + 840) % (2 * d - 2);
+        if (p + 1 == d) sl = K::ZEND + (d - 2) * (d - 1) + (a + 840) % (2 * d - 2);
       const bool last = p == S - 1;                             // x_S: global only
       const bool emit_s = last && inimg && a >= h0 && a < h1;
-      char* dst = rings + sl * ROWB + off * 2;
+      char* dst = rings + sl * ROWB + cf_off<SPR>(col + 1, off);
       const f32x4 m0 = *reinterpret_cast<const f32x4*>(bma + ch);
       const f32x4 i0 = *reinterpret_cast<const f32x4*>(bia + ch);
-      const char* src = inb + (8 * g) * 2;
       // the PT pixel tiles as independent accumulators, fragments read one
       // k-step ahead (same K order per tile as the GEMM)
       f32x4 acc[PT];
       bf16x8 bc[PT], bn[PT];
+      // chunk u = 4s + g of pixel pr: sub-plane 2s + g/2, unit 2 pr + g%2
+      int fb[PT];
+#pragma unroll
+      for (int j = 0; j < PT; ++j) {
+        int pr = min(16 * j + col, W - 1);
+        asm volatile("" : "+v"(pr));   // per step: not hoisted out of the row loop
+        fb[j] = ((g >> 1) * K::SPX + 2 * pr + (g & 1)) * 16;
+      }
+      auto frag = [&](int s, int j) __attribute__((always_inline)) {
+        return *reinterpret_cast<const bf16x8*>(inb + fb[j] + 2 * s * K::SPX * 16);
+      };
 #pragma unroll
       for (int j = 0; j < PT; ++j) {
         acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-        const int px = 16 * j + col;
-        const int pr = px < W ? px : W - 1;
-        bc[j] = *reinterpret_cast<const bf16x8*>(src + pr * K::ISTR);
+        bc[j] = frag(0, j);
       }
 #pragma unroll
       for (int s = 0; s < K::KSA; ++s) {
         if (s + 1 < K::KSA) {
 #pragma unroll
-          for (int j = 0; j < PT; ++j) {
-            const int px = 16 * j + col;
-            const int pr = px < W ? px : W - 1;
-            bn[j] = *reinterpret_cast<const bf16x8*>(src + pr * K::ISTR + 64 * (s + 1));
-          }
+          for (int j = 0; j < PT; ++j) bn[j] = frag(s + 1, j);
         }
 #pragma unroll
         for (int j = 0; j < PT; ++j) acc[j] = mfma_step(w1[s], bc[j], acc[j]);
@@ -812,7 +877,7 @@ __global__ __launch_bounds__((ChainFusedCfg<CI, WID, S, PT>::NT)) void chain_fus
         for (int e = 0; e < 4; ++e) o[e] = (bf16_t)fmaxf((acc[j][e] - m0[e]) * i0[e], 0.f);
         if (!inimg) o = bf16x4{};   // SAME padding rows of the chain
         if (px < W) {
-          if (!last) *reinterpret_cast<bf16x4*>(dst + (px + 1) * ASTR) = o;
+          if (!last) *reinterpret_cast<bf16x4*>(dst + 512 * j) = o;
           else if (emit_s)
             *reinterpret_cast<bf16x4*>(Bo + (img + (size_t)a * W + px) * q.ldb + ch) = o;
         }
@@ -826,50 +891,40 @@ __global__ __launch_bounds__((ChainFusedCfg<CI, WID, S, PT>::NT)) void chain_fus
       const int co = 16 * ci + 4 * g;
       const int r = a - 2 * k + 1;
       const bool inimg = r >= 0 && r < H;
-      const int zd = k == 1 ? 3 : 4;
-      const int zbase = k == 1 ? 0 : 3 + 4 * (k - 2);
-      // row offsets relative to the stage's z ring (< 64 KB: packed two per register)
-      const int rb0 = __builtin_amdgcn_readfirstlane(((r - 1 + 840) % zd) * ROWB);
-      const int rb1 = __builtin_amdgcn_readfirstlane(((r + 840) % zd) * ROWB);
-      const int rb2 = __builtin_amdgcn_readfirstlane(((r + 1 + 840) % zd) * ROWB);
-      const char* zring = rings + zbase * ROWB + col * ASTR;
+      // z_k ring (4 rows): tap row dy of output row r is ring row (r - 1 + dy) & 3
+      const char* zring = rings + 4 * (k - 1) * ROWB;
+      const int rbase = __builtin_amdgcn_readfirstlane(((r - 1 + 840) & 3) * ROWB);
       const bool chain_next = k < S - 1;
-      const int zsl = __builtin_amdgcn_readfirstlane((3 + 4 * (k - 1) + (r + 840) % 4) * ROWB);
+      const int zsl = __builtin_amdgcn_readfirstlane((4 * k + ((r + 840) & 3)) * ROWB);
       const int xsl = __builtin_amdgcn_readfirstlane(
-          (R::ZEND + (k - 1) * k + (r + 840) % (2 * k)) * ROWB);
+          (K::ZEND + (k - 1) * k + (r + 840) % (2 * k)) * ROWB);
       const f32x4 m = *reinterpret_cast<const f32x4*>(bmb + (k - 1) * 16 * WCO + co);
       const f32x4 sc = *reinterpret_cast<const f32x4*>(bib + (k - 1) * 16 * WCO + co);
       const bool emit = r >= h0 && r < h1;
       constexpr int KP = (KST + 1) / 2;
       unsigned bpk[KP];
+      {
+        const unsigned* kt = reinterpret_cast<const unsigned*>(ktl) + lane * KP;
 #pragma unroll
-      for (int s = 0; s < KST; ++s) {   // per-step tap offsets (no table kept live)
-        int kk = 32 * s + 8 * g;
-        asm volatile("" : "+v"(kk));
-        int dyi = 1, off = 0;
-        if (kk < R::KFLAT) {
-          const int tap = kk / WID, ch = kk - tap * WID;
-          dyi = tap / 3;
-          off = (tap % 3 - 1) * ASTR + ch * 2;
-        }
-        const unsigned rel = (dyi == 0 ? rb0 : (dyi == 1 ? rb1 : rb2)) + off + ASTR;
-        if (s & 1) bpk[s >> 1] |= rel << 16;
-        else bpk[s >> 1] = rel;
+        for (int i = 0; i < KP; ++i) bpk[i] = kt[i];
       }
       auto boff = [&](int s) __attribute__((always_inline)) {
-        return (s & 1) ? (bpk[s >> 1] >> 16) : (bpk[s >> 1] & 0xFFFFu);
+        const int e = (s & 1) ? (int)(bpk[s >> 1] >> 16) : (int)(bpk[s >> 1] & 0xFFFFu);
+        const int v = rbase + e;
+        return v >= 4 * ROWB ? v - 4 * ROWB : v;
       };
-      auto epilogue = [&](const f32x4& acc, int px) __attribute__((always_inline)) {
+      const int pxo = cf_off<SPR>(col + 1, co);   // this lane's 4 channels, tile 0
+      auto epilogue = [&](const f32x4& acc, int j) __attribute__((always_inline)) {
+        const int px = 16 * j + col;
         if (!(co < WID && px < W)) return;
-        const int pxo = px * ASTR + co * 2 + ASTR;
         bf16x4 y;
 #pragma unroll
         for (int e = 0; e < 4; ++e) y[e] = (bf16_t)fmaxf((acc[e] - m[e]) * sc[e], 0.f);
         if (emit)
           *reinterpret_cast<bf16x4*>(Bo + (img + (size_t)r * W + px) * q.ldb + (k - 1) * WID + co) = y;
         if (chain_next) {
-          const bf16x4 x = *reinterpret_cast<const bf16x4*>(rings + xsl + pxo);
-          *reinterpret_cast<bf16x4*>(rings + zsl + pxo) = inimg ? add4(x, y) : bf16x4{};
+          const bf16x4 x = *reinterpret_cast<const bf16x4*>(rings + xsl + pxo + 512 * j);
+          *reinterpret_cast<bf16x4*>(rings + zsl + pxo + 512 * j) = inimg ? add4(x, y) : bf16x4{};
         }
       };
       f32x4 acc[PT];
@@ -877,14 +932,14 @@ __global__ __launch_bounds__((ChainFusedCfg<CI, WID, S, PT>::NT)) void chain_fus
 #pragma unroll
       for (int j = 0; j < PT; ++j) {
         acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-        bc[j] = *reinterpret_cast<const bf16x8*>(zring + boff(0) + 16 * j * ASTR);
+        bc[j] = *reinterpret_cast<const bf16x8*>(zring + boff(0) + 512 * j);
       }
 #pragma unroll
       for (int s = 0; s < KST; ++s) {
         if (s + 1 < KST) {
 #pragma unroll
           for (int j = 0; j < PT; ++j)
-            bn[j] = *reinterpret_cast<const bf16x8*>(zring + boff(s + 1) + 16 * j * ASTR);
+            bn[j] = *reinterpret_cast<const bf16x8*>(zring + boff(s + 1) + 512 * j);
         }
 #pragma unroll
         for (int j = 0; j < PT; ++j) acc[j] = mfma_step(wb[s], bc[j], acc[j]);
@@ -893,7 +948,7 @@ __global__ __launch_bounds__((ChainFusedCfg<CI, WID, S, PT>::NT)) void chain_fus
         __builtin_amdgcn_sched_barrier(0);   // reads stay one k-step ahead
       }
 #pragma unroll
-      for (int j = 0; j < PT; ++j) epilogue(acc[j], 16 * j + col);
+      for (int j = 0; j < PT; ++j) epilogue(acc[j], j);
     }
     __syncthreads();
   }
@@ -990,7 +1045,8 @@ __global__ __launch_bounds__((SplitS2Cfg<WID, S, WIN>::NT)) void split_s2_rows(C
   constexpr int NT = K::NT, WCO = K::WCO, KST = K::KST, ASTR = K::ASTR, CU = K::CU;
   constexpr int PT = K::PT, W = WIN, Wo = K::WOUT, ROWB = K::WR * ASTR, PLANEB = 3 * ROWB;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: scalar ring math
   const int col = lane & 15, g = lane >> 4;
   const int H = q.H;
   const int Ho = (H + 1) / 2;
