@@ -19,7 +19,7 @@
 //   phase 1 : every 3x3 stage k at once, on row a-2k+1 (ring z_k rows
 //             a-2k..a-2k+2, all written in earlier steps or phase 0)
 //             -> ring y_k, and z_{k+1} = x_{k+1} + y_k (bf16, as unfused)
-// Ring depths follow from the lags: z_1 3 rows, z_k 4, x_k 2k-2, x_S 2S-1,
+// Ring depths follow from the lags: z_k 4 rows, x_k 2k-2, x_S 2S-1,
 // y_k 2S-1-2k.  Rows outside the image are zero (SAME padding).  Segments
 // recompute 3(S-1) warm-up rows.
 //
@@ -56,9 +56,9 @@ struct BneckCfg {
   static constexpr int WR = 16 * PT + 2;  // ring row: pad | pixels | pad (+ tile slack)
   static constexpr int ROWB = WR * ASTR;
   // ring planes (one image row each) and depths
-  static constexpr int ZD(int k) { return k == 1 ? 3 : 4; }
-  static constexpr int ZB(int k) { return k == 1 ? 0 : 3 + 4 * (k - 2); }   // z_k, k = 1..S-1
-  static constexpr int ZEND = 3 + 4 * (S - 2);
+  // z_k: 4 rows each (k = 1..S-1), so a stage's three tap rows wrap with a mask
+  static constexpr int ZB(int k) { return 4 * (k - 1); }
+  static constexpr int ZEND = 4 * (S - 1);
   static constexpr int XD(int k) { return k == S ? 2 * S - 1 : 2 * k - 2; }
   static constexpr int XB(int k) { return ZEND + (k - 2) * (k - 1); }       // x_k, k = 2..S
   static constexpr int XEND = XB(S) + 2 * S - 1;
@@ -69,7 +69,11 @@ struct BneckCfg {
   static constexpr int RING_BYTES = NPLANES * ROWB;
   static constexpr int IN_BYTES = 16 * PT * ISTR;
   static constexpr int BN_FLOATS = 2 * (S - 1) * 16 * WCO + 2 * SW + 2 * C + (PROJ ? 2 * C : 0);
-  static constexpr int LDS = RING_BYTES + IN_BYTES + 4 * BN_FLOATS;
+  static constexpr int KP = (KST + 1) / 2;
+  static constexpr int KTB = 64 * KP * 4;   // tap table [lane][k-step] u16
+  static constexpr int LDS = RING_BYTES + IN_BYTES + KTB + 4 * BN_FLOATS;
+  static_assert(4 * ROWB < 65536, "tap offsets in 16 bits");
+  static_assert(LDS <= 163840, "LDS");
   static constexpr int CU = CI / 8;                           // 16-B chunks per input pixel
   static constexpr int IREG = (16 * PT * CU + NT - 1) / NT;   // input-row chunks per thread
 };
@@ -100,7 +104,8 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
   const int h1 = min(H, h0 + q.seg);
   char* rings = smem;
   char* inb = smem + K::RING_BYTES;
-  float* bmb = reinterpret_cast<float*>(inb + K::IN_BYTES);   // [S-1][16*WCO]
+  unsigned short* ktl = reinterpret_cast<unsigned short*>(inb + K::IN_BYTES);
+  float* bmb = reinterpret_cast<float*>(inb + K::IN_BYTES + K::KTB);   // [S-1][16*WCO]
   float* bib = bmb + (S - 1) * 16 * WCO;
   float* bma = bib + (S - 1) * 16 * WCO;                      // 1x1a BN [SW]
   float* bia = bma + K::SW;
@@ -170,18 +175,18 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
                   ? ld16(Wk + (size_t)(ci * 16 + col) * K::KFLAT + kk) : bf16x8{};
     }
   }
-  // k-step table of this lane group: tap row (0..2) << 24 | (byte offset + 2^15)
-  int ktab[KST];
-#pragma unroll
-  for (int s = 0; s < KST; ++s) {
-    const int kk = 32 * s + 8 * g;
+  // tap table: for lane l and k-step s, the byte offset of its B fragment (pixel
+  // tile 0) in a 4-row z ring, counted from the ring row of tap row 0
+  for (int e = tid; e < 64 * KST; e += NT) {
+    const int l = e / KST, st = e - l * KST;
+    const int kk = 32 * st + 8 * (l >> 4);
     int dyi = 1, off = 0;
     if (kk < K::KFLAT) {
       const int tap = kk / WID, ch = kk - tap * WID;
       dyi = tap / 3;
       off = (tap % 3 - 1) * ASTR + ch * 2;
     }
-    ktab[s] = (dyi << 24) | (off + 32768);
+    ktl[l * K::KP * 2 + st] = (unsigned short)(dyi * ROWB + off + ASTR + (l & 15) * ASTR);
   }
 
   // ---- input rows: global -> registers (prefetch) -> LDS
@@ -242,7 +247,7 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
       const bool inimg = a >= 0 && a < H;
       const int ch = 32 * pq + 8 * g;
       const int p = ch / WID, off = ch - p * WID;
-      int sl = K::ZB(1) + slot<3>(a);                // plane 0 -> z_1 = x_1
+      int sl = K::ZB(1) + (a & 3);                   // plane 0 -> z_1 = x_1
 #pragma unroll
       for (int d = 2; d <= S; ++d)
         if (p + 1 == d) sl = K::XB(d) + (a + 840) % K::XD(d);
@@ -255,9 +260,10 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
         bf16x8 o;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          o[e] = (bf16_t)fmaxf((acc0[e] - m0[e]) * i0[e], 0.f);
-          o[4 + e] = (bf16_t)fmaxf((acc1[e] - m1[e]) * i1[e], 0.f);
+          o[e] = (bf16_t)((acc0[e] - m0[e]) * i0[e]);
+          o[4 + e] = (bf16_t)((acc1[e] - m1[e]) * i1[e]);
         }
+        o = relu_bf16(o);
         if (!inimg) o = bf16x8{};
         if (px < W) *reinterpret_cast<bf16x8*>(dst + (px + 1) * ASTR) = o;
       };
@@ -326,9 +332,10 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
 #pragma clang fp contract(off)
           float v0 = (acc0[e] - m0[e]) * i0[e] + (float)rv[e];
           float v1 = (acc1[e] - m1[e]) * i1[e] + (float)rv[4 + e];
-          o[e] = (bf16_t)fmaxf(v0, 0.f);
-          o[4 + e] = (bf16_t)fmaxf(v1, 0.f);
+          o[e] = (bf16_t)v0;
+          o[4 + e] = (bf16_t)v1;
         }
+        o = relu_bf16(o);
         if (px < W) *reinterpret_cast<bf16x8*>(Y + (img + (size_t)c * W + px) * C + ch) = o;
       };
 #pragma unroll
@@ -367,35 +374,38 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
       const int co = 16 * ci + 4 * g;
       const int r = a - 2 * k + 1;
       const bool inimg = r >= 0 && r < H;
-      // ring geometry of stage k (wave-uniform -> scalar registers)
-      const int zd = k == 1 ? 3 : 4;
-      const int zbase = k == 1 ? 0 : 3 + 4 * (k - 2);
-      const int rb0 = __builtin_amdgcn_readfirstlane((zbase + (r - 1 + 840) % zd) * ROWB);
-      const int rb1 = __builtin_amdgcn_readfirstlane((zbase + (r + 840) % zd) * ROWB);
-      const int rb2 = __builtin_amdgcn_readfirstlane((zbase + (r + 1 + 840) % zd) * ROWB);
+      // ring geometry of stage k (wave-uniform -> scalar registers); tap row dy
+      // of output row r is ring row (r - 1 + dy) & 3 of z_k
+      const char* zring = rings + K::ZB(k) * ROWB;
+      const int rbase = __builtin_amdgcn_readfirstlane(((r - 1 + 840) & 3) * ROWB);
       const int ysl = __builtin_amdgcn_readfirstlane(
           (K::XEND + (k - 1) * (2 * S - 1 - k) + (r + 840) % (2 * S - 1 - 2 * k)) * ROWB);
       const bool chain_next = k < S - 1;
-      const int zsl = __builtin_amdgcn_readfirstlane((3 + 4 * (k - 1) + (r + 840) % 4) * ROWB);
+      const int zsl = __builtin_amdgcn_readfirstlane((K::ZB(k + 1) + ((r + 840) & 3)) * ROWB);
       const int xsl = __builtin_amdgcn_readfirstlane(
           (K::ZEND + (k - 1) * k + (r + 840) % (2 * k)) * ROWB);
       const f32x4 m = *reinterpret_cast<const f32x4*>(bmb + (k - 1) * 16 * WCO + co);
       const f32x4 sc = *reinterpret_cast<const f32x4*>(bib + (k - 1) * 16 * WCO + co);
-      // per-lane B offsets of the k-steps for the three tap rows
+      unsigned bpk[K::KP];
+      {
+        const unsigned* kt = reinterpret_cast<const unsigned*>(ktl) + lane * K::KP;
+#pragma unroll
+        for (int i = 0; i < K::KP; ++i) bpk[i] = kt[i];
+      }
       int boff[KST];
 #pragma unroll
       for (int s = 0; s < KST; ++s) {
-        int e = ktab[s];
-        asm volatile("" : "+v"(e));  // keep the select in the loop body (no hoisting)
-        const int dyi = e >> 24;
-        boff[s] = (dyi == 0 ? rb0 : (dyi == 1 ? rb1 : rb2)) + (e & 0xFFFFFF) - 32768 + ASTR;
+        const int e = (s & 1) ? (int)(bpk[s >> 1] >> 16) : (int)(bpk[s >> 1] & 0xFFFFu);
+        const int v = rbase + e;
+        boff[s] = v >= 4 * ROWB ? v - 4 * ROWB : v;
       }
       auto epilogue = [&](const f32x4& acc, int px) __attribute__((always_inline)) {
         if (!(co < WID && px < W)) return;
         const int pxo = px * ASTR + co * 2 + ASTR;
         bf16x4 y;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) y[e] = (bf16_t)fmaxf((acc[e] - m[e]) * sc[e], 0.f);
+        for (int e = 0; e < 4; ++e) y[e] = (bf16_t)((acc[e] - m[e]) * sc[e]);
+        y = relu_bf16(y);
         if (!inimg) y = bf16x4{};
         *reinterpret_cast<bf16x4*>(rings + ysl + pxo) = y;
         if (chain_next) {
@@ -410,8 +420,8 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
         bf16x8 b0[KST], b1[KST];
 #pragma unroll
         for (int s = 0; s < KST; ++s) {
-          b0[s] = *reinterpret_cast<const bf16x8*>(rings + boff[s] + px0 * ASTR);
-          b1[s] = two ? *reinterpret_cast<const bf16x8*>(rings + boff[s] + px1 * ASTR) : bf16x8{};
+          b0[s] = *reinterpret_cast<const bf16x8*>(zring + boff[s] + 16 * j * ASTR);
+          b1[s] = two ? *reinterpret_cast<const bf16x8*>(zring + boff[s] + 16 * (j + 1) * ASTR) : bf16x8{};
         }
         f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -624,7 +634,8 @@ __global__ __launch_bounds__((ChainRowsCfg<WID, S, PT>::NT)) void chain_rows(Cha
         const int pxo = px * ASTR + co * 2 + ASTR;
         bf16x4 y;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) y[e] = (bf16_t)fmaxf((acc[e] - m[e]) * sc[e], 0.f);
+        for (int e = 0; e < 4; ++e) y[e] = (bf16_t)((acc[e] - m[e]) * sc[e]);
+        y = relu_bf16(y);
         if (emit)
           *reinterpret_cast<bf16x4*>(Bo + (img + (size_t)r * W + px) * q.ldb + (k - 1) * WID + co) = y;
         if (chain_next) {
@@ -874,7 +885,8 @@ __global__ __launch_bounds__((ChainFusedCfg<CI, WID, S, PT>::NT)) void chain_fus
         const int px = 16 * j + col;
         bf16x4 o;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = (bf16_t)fmaxf((acc[j][e] - m0[e]) * i0[e], 0.f);
+        for (int e = 0; e < 4; ++e) o[e] = (bf16_t)((acc[j][e] - m0[e]) * i0[e]);
+        o = relu_bf16(o);
         if (!inimg) o = bf16x4{};   // SAME padding rows of the chain
         if (px < W) {
           if (!last) *reinterpret_cast<bf16x4*>(dst + 512 * j) = o;
@@ -919,7 +931,8 @@ __global__ __launch_bounds__((ChainFusedCfg<CI, WID, S, PT>::NT)) void chain_fus
         if (!(co < WID && px < W)) return;
         bf16x4 y;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) y[e] = (bf16_t)fmaxf((acc[e] - m[e]) * sc[e], 0.f);
+        for (int e = 0; e < 4; ++e) y[e] = (bf16_t)((acc[e] - m[e]) * sc[e]);
+        y = relu_bf16(y);
         if (emit)
           *reinterpret_cast<bf16x4*>(Bo + (img + (size_t)r * W + px) * q.ldb + (k - 1) * WID + co) = y;
         if (chain_next) {
@@ -1164,7 +1177,8 @@ __global__ __launch_bounds__((SplitS2Cfg<WID, S, WIN>::NT)) void split_s2_rows(C
         if (!(co < WID && wo < Wo)) return;
         bf16x4 y;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) y[e] = (bf16_t)fmaxf((acc[e] - m[e]) * sc[e], 0.f);
+        for (int e = 0; e < 4; ++e) y[e] = (bf16_t)((acc[e] - m[e]) * sc[e]);
+        y = relu_bf16(y);
         *reinterpret_cast<bf16x4*>(Bo + (imgo + (size_t)ho * Wo + wo) * q.ldb + ck * WID + co) = y;
       };
       for (int j = 0; j < PT; j += 2) {
@@ -1407,7 +1421,8 @@ __global__ __launch_bounds__((S2FusedCfg<CI, WID, S, WIN>::NT)) void s2_fused(Ch
           for (int s = 0; s < K::KSA; ++s) a0 = mfma_step(w1[s], b[s], a0);
           bf16x4 o;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) o[e] = (bf16_t)fmaxf((a0[e] - m0[e]) * i0[e], 0.f);
+          for (int e = 0; e < 4; ++e) o[e] = (bf16_t)((a0[e] - m0[e]) * i0[e]);
+          o = relu_bf16(o);
           if (!inimg) o = bf16x4{};   // the fixed zero padding of the stride-2 convs
           if (px < W) *reinterpret_cast<bf16x4*>(dst + (px + 1) * ASTR) = o;
           __builtin_amdgcn_sched_barrier(0);
@@ -1453,7 +1468,8 @@ __global__ __launch_bounds__((S2FusedCfg<CI, WID, S, WIN>::NT)) void s2_fused(Ch
           if (co < WID && wo < Wo) {
             bf16x4 y;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) y[e] = (bf16_t)fmaxf((acc[e] - m[e]) * sc[e], 0.f);
+            for (int e = 0; e < 4; ++e) y[e] = (bf16_t)((acc[e] - m[e]) * sc[e]);
+            y = relu_bf16(y);
             *reinterpret_cast<bf16x4*>(Bo + (imgo + (size_t)ho * Wo + wo) * q.ldb + ck * WID + co) = y;
           }
         }

@@ -28,6 +28,22 @@ __device__ __forceinline__ bf16x8 frag_add(bf16x8 a, bf16x8 b) {
 }
 __device__ __forceinline__ f32x4 frag_add(f32x4 a, f32x4 b) { return a + b; }
 
+// ReLU on bf16 bit patterns: every negative value (and -0) has the sign bit
+// set, i.e. is a negative int16, so a packed int16 max with 0 is ReLU.  bf16
+// rounding is monotone and keeps the sign, so relu(bf16(x)) == bf16(relu(x))
+// bit for bit; one v_pk_max_i16 per two channels instead of two v_max_f32.
+__device__ __forceinline__ bf16x4 relu_bf16(bf16x4 v) {
+  typedef short s16x4 __attribute__((ext_vector_type(4)));
+  const s16x4 s = __builtin_elementwise_max(__builtin_bit_cast(s16x4, v), (s16x4){0, 0, 0, 0});
+  return __builtin_bit_cast(bf16x4, s);
+}
+__device__ __forceinline__ bf16x8 relu_bf16(bf16x8 v) {
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  const s16x8 s = __builtin_elementwise_max(__builtin_bit_cast(s16x8, v),
+                                            (s16x8){0, 0, 0, 0, 0, 0, 0, 0});
+  return __builtin_bit_cast(bf16x8, s);
+}
+
 __device__ __forceinline__ f32x4 mfma_step(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
