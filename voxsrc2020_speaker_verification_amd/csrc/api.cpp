@@ -977,6 +977,7 @@ static int build_res2net(Builder& B, const float* x, int n, int t, float* out) {
             q.inv[j] = (const float*)br.inv->p;
           }
           q.lds = s2_fused_lds(cur.C, w, s, W);
+          q.dbg = m->bneck_dbg;
           Op op;
           op.kind = OP_CONV;
           op.type = 22;
@@ -1014,6 +1015,7 @@ static int build_res2net(Builder& B, const float* x, int n, int t, float* out) {
             q.inv[j] = (const float*)br.inv->p;
           }
           q.lds = chain_fused_lds(cur.C, w, s, W);
+          q.dbg = m->bneck_dbg;
           Op op;
           op.kind = OP_CONV;
           op.type = 24;

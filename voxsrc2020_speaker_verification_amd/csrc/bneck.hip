@@ -1271,14 +1271,21 @@ struct S2FusedCfg {
   static constexpr int KST = (KFLAT + 31) / 32;
   static constexpr int AU = ((WID / 8) & 1) ? WID / 8 : WID / 8 + 1;
   static constexpr int ASTR = AU * 16;
-  static constexpr int IU = ((CI / 8) & 1) ? CI / 8 : CI / 8 + 1;
-  static constexpr int ISTR = IU * 16;           // staged input pixel stride
+  // staged input rows: chunk u (8 channels) of pixel px at 16-B unit
+  // (u/2) SPX + 2 px + u%2 -- the two lane groups a ds_read_b128 pairs read
+  // chunks u, u+1 of 8 distinct pixels: opposite parities, conflict-free
+  // (SPX = 2 mod 8 keeps the 8-lane store groups conflict-free too)
+  static constexpr int CU = CI / 8;
+  static constexpr int SPX = 2 * WIN + 2;
   static constexpr int ROWB = WR * ASTR, PLANEB = 3 * ROWB;
   static constexpr int RING = S * PLANEB;
-  static constexpr int INROW = WIN * ISTR;
-  static constexpr int CU = CI / 8;
+  static constexpr int INROW = CU / 2 * SPX * 16;
+  static_assert(SPX % 8 == 2 && CU % 2 == 0, "staging layout");
   static constexpr int XREG = (2 * WIN * CU + NT - 1) / NT;   // two input rows per step
-  static constexpr int LDS = RING + 2 * INROW + 4 * (2 * (S - 1) * 16 * WCO + 2 * SW) + 4 * 4 * KST;
+  static constexpr int KP = (KST + 1) / 2;
+  static constexpr int KTB = 64 * KP * 4;        // tap table [lane][k-step] u16
+  static constexpr int LDS = RING + 2 * INROW + 4 * (2 * (S - 1) * 16 * WCO + 2 * SW) + KTB;
+  static_assert(3 * ROWB + 2 * ROWB < 65536, "tap offsets in 16 bits");
 };
 
 template <int CI, int WID, int S, int WIN>
@@ -1304,7 +1311,7 @@ __global__ __launch_bounds__((S2FusedCfg<CI, WID, S, WIN>::NT)) void s2_fused(Ch
   float* bib = bmb + (S - 1) * 16 * WCO;
   float* bma = bib + (S - 1) * 16 * WCO;          // 1x1a BN [SW]
   float* bia = bma + K::SW;
-  int* ktab_l = reinterpret_cast<int*>(bia + K::SW);   // [4 lane groups][KST]
+  unsigned short* ktl = reinterpret_cast<unsigned short*>(bia + K::SW);
   const bf16_t* __restrict__ X = reinterpret_cast<const bf16_t*>(q.x);
   bf16_t* __restrict__ Bo = reinterpret_cast<bf16_t*>(q.b);
   const size_t img = (size_t)n * H * W;
@@ -1351,16 +1358,19 @@ __global__ __launch_bounds__((S2FusedCfg<CI, WID, S, WIN>::NT)) void s2_fused(Ch
     for (int s = 0; s < K::KSA; ++s)
       w1[s] = ld16(Wa + (size_t)(t16 * 16 + col) * CI + 32 * s + 8 * g);
   }
-  for (int i = tid; i < 4 * KST; i += NT) {
-    const int gg = i / KST, s = i - gg * KST;
-    const int kk = 32 * s + 8 * gg;
+  // tap table: for lane l and k-step s, the byte offset of its B fragment
+  // (output pixel tile 0, stride-2 column 2 col) in the 3-row ring of a plane,
+  // counted from the ring row of tap row 0 (before wrapping)
+  for (int e = tid; e < 64 * KST; e += NT) {
+    const int l = e / KST, st = e - l * KST;
+    const int kk = 32 * st + 8 * (l >> 4);
     int dyi = 1, off = 0;
     if (kk < K::KFLAT) {
       const int tap = kk / WID, ch = kk - tap * WID;
       dyi = tap / 3;
       off = (tap % 3 - 1) * ASTR + ch * 2;
     }
-    ktab_l[i] = (dyi << 24) | (off + 32768);
+    ktl[l * K::KP * 2 + st] = (unsigned short)(dyi * ROWB + off + ASTR + 2 * (l & 15) * ASTR);
   }
 
   // two input rows per step: global -> registers (one step ahead) -> LDS
@@ -1387,7 +1397,8 @@ __global__ __launch_bounds__((S2FusedCfg<CI, WID, S, WIN>::NT)) void s2_fused(Ch
       asm volatile("" : "+v"(c));
       const int rr = c / (W * CU), cc = c - rr * (W * CU);
       const int px = cc / CU, u = cc - px * CU;
-      if (rr < 2) *reinterpret_cast<uint4*>(inb + rr * K::INROW + px * K::ISTR + u * 16) = xr[i];
+      if (rr < 2)
+        *reinterpret_cast<uint4*>(inb + rr * K::INROW + ((u >> 1) * K::SPX + 2 * px + (u & 1)) * 16) = xr[i];
     }
   };
 
@@ -1395,43 +1406,55 @@ __global__ __launch_bounds__((S2FusedCfg<CI, WID, S, WIN>::NT)) void s2_fused(Ch
   store_x();
   __syncthreads();
   for (int ho = g0 - 1; ho < g1; ++ho) {
-    load_x(2 * ho + 2);   // lands during this step, goes to LDS at its end
+    if (!(q.dbg & 8)) load_x(2 * ho + 2);   // lands during this step, goes to LDS at its end
     // ---------------- phase A: 1x1a rows 2ho, 2ho+1 -> ring
-    {
+    if (!(q.dbg & 1)) {
       const int ch = 32 * (t16 >> 1) + 8 * g + 4 * (t16 & 1);
       const int p = ch / WID, off = ch - p * WID;
       const f32x4 m0 = *reinterpret_cast<const f32x4*>(bma + ch);
       const f32x4 i0 = *reinterpret_cast<const f32x4*>(bia + ch);
+      // the 2 x PTI (row, pixel tile) items in sequence, the next item's
+      // fragments read before this item's MFMAs
+      constexpr int NI = 2 * K::PTI;
+      // chunk u = 4s + g of pixel pr: sub-plane 2s + g/2, unit 2 pr + g%2
+      const int gb = ((g >> 1) * K::SPX + (g & 1)) * 16;
+      auto frag = [&](int it, int s) __attribute__((always_inline)) {
+        const int rr = it / K::PTI, j = it - rr * K::PTI;
+        int pr = min(16 * j + col, W - 1);
+        asm volatile("" : "+v"(pr));   // item bases are not hoisted out of the row loop
+        return *reinterpret_cast<const bf16x8*>(inb + rr * K::INROW + gb + 32 * pr + 2 * s * K::SPX * 16);
+      };
+      bf16x8 bc[K::KSA], bn[K::KSA];
 #pragma unroll
-      for (int rr = 0; rr < 2; ++rr) {
+      for (int s = 0; s < K::KSA; ++s) bc[s] = frag(0, s);
+#pragma unroll
+      for (int it = 0; it < NI; ++it) {
+        const int rr = it / K::PTI, j = it - rr * K::PTI;
+        if (it + 1 < NI) {
+#pragma unroll
+          for (int s = 0; s < K::KSA; ++s) bn[s] = frag(it + 1, s);
+        }
+        f32x4 a0 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < K::KSA; ++s) a0 = mfma_step(w1[s], bc[s], a0);
         const int r = 2 * ho + rr;
         const bool inimg = r >= 0 && r < H;
         char* dst = rings + p * PLANEB + ((r + 840) % 3) * ROWB + off * 2;
-        const char* src = inb + rr * K::INROW + (8 * g) * 2;
+        const int px = 16 * j + col;
+        bf16x4 o;
 #pragma unroll
-        for (int j = 0; j < K::PTI; ++j) {
-          const int px = 16 * j + col;
-          const int pr = px < W ? px : W - 1;
-          bf16x8 b[K::KSA];
+        for (int e = 0; e < 4; ++e) o[e] = (bf16_t)((a0[e] - m0[e]) * i0[e]);
+        o = relu_bf16(o);
+        if (!inimg) o = bf16x4{};   // the fixed zero padding of the stride-2 convs
+        if (px < W) *reinterpret_cast<bf16x4*>(dst + (px + 1) * ASTR) = o;
 #pragma unroll
-          for (int s = 0; s < K::KSA; ++s)
-            b[s] = *reinterpret_cast<const bf16x8*>(src + pr * K::ISTR + 64 * s);
-          f32x4 a0 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int s = 0; s < K::KSA; ++s) a0 = mfma_step(w1[s], b[s], a0);
-          bf16x4 o;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) o[e] = (bf16_t)((a0[e] - m0[e]) * i0[e]);
-          o = relu_bf16(o);
-          if (!inimg) o = bf16x4{};   // the fixed zero padding of the stride-2 convs
-          if (px < W) *reinterpret_cast<bf16x4*>(dst + (px + 1) * ASTR) = o;
-          __builtin_amdgcn_sched_barrier(0);
-        }
+        for (int s = 0; s < K::KSA; ++s) bc[s] = bn[s];
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
     __syncthreads();
     // ---------------- phase B: output row ho from A-rows 2ho-1 .. 2ho+1
-    if (ho >= g0) {
+    if (ho >= g0 && !(q.dbg & 2)) {
       const int rb0 = __builtin_amdgcn_readfirstlane(((2 * ho - 1 + 840) % 3) * ROWB);
       const int rb1 = __builtin_amdgcn_readfirstlane(((2 * ho + 840) % 3) * ROWB);
       const int rb2 = __builtin_amdgcn_readfirstlane(((2 * ho + 1 + 840) % 3) * ROWB);
@@ -1440,40 +1463,52 @@ __global__ __launch_bounds__((S2FusedCfg<CI, WID, S, WIN>::NT)) void s2_fused(Ch
         const char* zb = rings + ck * PLANEB;
         const f32x4 m = *reinterpret_cast<const f32x4*>(bmb + ck * 16 * WCO + co);
         const f32x4 sc = *reinterpret_cast<const f32x4*>(bib + ck * 16 * WCO + co);
-        int boff[KST];
+        unsigned bpk[K::KP];
+        {
+          const unsigned* kt = reinterpret_cast<const unsigned*>(ktl) + lane * K::KP;
+#pragma unroll
+          for (int i = 0; i < K::KP; ++i) bpk[i] = kt[i];
+        }
+        auto boff = [&](int s) __attribute__((always_inline)) {
+          const int e = (s & 1) ? (int)(bpk[s >> 1] >> 16) : (int)(bpk[s >> 1] & 0xFFFFu);
+          const int v = rb0 + e;
+          return v >= 3 * ROWB ? v - 3 * ROWB : v;
+        };
+        // the PTO output tiles as independent accumulators, fragments one k-step
+        // ahead (columns past Wo read the row's tail / the next row: discarded)
+        constexpr int PT = K::PTO;
+        f32x4 acc[PT];
+        bf16x8 bc[PT], bn[PT];
+#pragma unroll
+        for (int j = 0; j < PT; ++j) {
+          acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+          bc[j] = *reinterpret_cast<const bf16x8*>(zb + boff(0) + 32 * j * ASTR);
+        }
 #pragma unroll
         for (int s = 0; s < KST; ++s) {
-          int e = ktab_l[g * KST + s];
-          const int dyi = e >> 24;
-          boff[s] = (dyi == 0 ? rb0 : (dyi == 1 ? rb1 : rb2)) + (e & 0xFFFFFF) - 32768 + ASTR;
-        }
-#pragma unroll 1
-        for (int j = 0; j < K::PTO; ++j) {
-          const int wo = 16 * j + col;
-          const int wr = 2 * (wo < Wo ? wo : Wo - 1) * ASTR;
-          f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-          constexpr int KH = (KST + 2) / 3;   // B fragments in thirds (register budget)
+          if (s + 1 < KST) {
 #pragma unroll
-          for (int h = 0; h < 3; ++h) {
-            bf16x8 b0[KH];
-#pragma unroll
-            for (int i = 0; i < KH; ++i)
-              if (h * KH + i < KST)
-                b0[i] = *reinterpret_cast<const bf16x8*>(zb + boff[h * KH + i] + wr);
-#pragma unroll
-            for (int i = 0; i < KH; ++i)
-              if (h * KH + i < KST) acc = mfma_step(wb[h * KH + i], b0[i], acc);
-            __builtin_amdgcn_sched_barrier(0);   // one third of the fragments live at a time
+            for (int j = 0; j < PT; ++j)
+              bn[j] = *reinterpret_cast<const bf16x8*>(zb + boff(s + 1) + 32 * j * ASTR);
           }
+#pragma unroll
+          for (int j = 0; j < PT; ++j) acc[j] = mfma_step(wb[s], bc[j], acc[j]);
+#pragma unroll
+          for (int j = 0; j < PT; ++j) bc[j] = bn[j];
+          __builtin_amdgcn_sched_barrier(0);   // reads stay one k-step ahead
+        }
+#pragma unroll
+        for (int j = 0; j < PT; ++j) {
+          const int wo = 16 * j + col;
           if (co < WID && wo < Wo) {
             bf16x4 y;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) y[e] = (bf16_t)((acc[e] - m[e]) * sc[e]);
+            for (int e = 0; e < 4; ++e) y[e] = (bf16_t)((acc[j][e] - m[e]) * sc[e]);
             y = relu_bf16(y);
             *reinterpret_cast<bf16x4*>(Bo + (imgo + (size_t)ho * Wo + wo) * q.ldb + ck * WID + co) = y;
           }
         }
-      } else {
+      } else if (!(q.dbg & 4)) {
         // last split: AvgPool 3x3/2 VALID over the fixed-padded plane, divisor 9
         // (taps outside the image skipped, in the order of avgpool3s2_v8)
         const char* pl = rings + (S - 1) * PLANEB;
@@ -1502,7 +1537,7 @@ __global__ __launch_bounds__((S2FusedCfg<CI, WID, S, WIN>::NT)) void s2_fused(Ch
         }
       }
     }
-    store_x();   // input rows 2ho+2, 2ho+3 (phase A of this step is done with the staging)
+    if (!(q.dbg & 8)) store_x();   // input rows 2ho+2, 2ho+3 (phase A of this step is done with the staging)
     __syncthreads();
   }
 }

@@ -61,6 +61,7 @@ struct ChainParams {
   // s2_fused only: the block input and its 1x1a (paired-row weights + BN)
   const void* x; int ldx; int cin;
   const void* wa; const float* ma; const float* ia;
+  int dbg;                          // diagnostics (VOXEMB_BNECK_DBG): skip parts, garbage out
 };
 hipError_t launch_split_chain(const ChainParams& q, int wco, int wpx, hipStream_t s);
 // Row-streamed split chain (bneck.hip): utterance segments of q.R rows, q.nwaves
