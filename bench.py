@@ -35,6 +35,8 @@ def _kernel_name(tag, dt):
     if tag & (1 << 30):
         return "gemm1x1_wide"
     if tag & (1 << 29):
+        if tag & (1 << 18):
+            return "conv3x3_rw"
         return "conv3x3_win" if tag & (1 << 19) else "conv3x3_pipe"
     if tag & (1 << 28):
         return "gconv3x3_rows"

@@ -396,6 +396,31 @@ def test_chain_fused_bitwise(weights, name, F, T, N, monkeypatch):
                                         ("res2net50_w24_s4_c32", 80, 123, 7),
                                         ("res2net50_w24_s4_c32", 40, 75, 3),
                                         ("res2net50_w24_s4_c32", 40, 37, 2),
+                                        ("res2net50_w24_s4_c32", 80, 27, 1),
+                                        ("res2net101_w24_s4_c32_att", 80, 64, 3)])
+def test_conv3_rw_bitwise_pipe(weights, name, F, T, N, monkeypatch):
+    """The register-weight 3x3 (weights resident in registers, each
+    utterance-aligned 128-pixel tile's input window staged once in LDS, the
+    next branch's addend formed in place from LDS-staged x rows; ragged last
+    tiles, short utterances) gives the same bits as conv3x3_pipe."""
+    import torch
+    from voxsrc2020_speaker_verification_amd import synth
+    spec, t, blob = weights(name, F)
+    x = synth.make_features(N, T, F, seed=41)
+    with _extractor(blob, "bf16") as ex:
+        got = ex.run(x)
+        assert sum(l.startswith("conv3rw") for l in ex.describe(torch.from_numpy(x).cuda())) >= 6
+    monkeypatch.setenv("VOXEMB_NO_CONV3_RW", "1")
+    with _extractor(blob, "bf16") as ex:
+        ref = ex.run(x)
+        assert not any(l.startswith("conv3rw") for l in ex.describe(torch.from_numpy(x).cuda()))
+    assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("name,F,T,N", [("res2net50_w24_s4_c32", 80, 200, 16),
+                                        ("res2net50_w24_s4_c32", 80, 123, 7),
+                                        ("res2net50_w24_s4_c32", 40, 75, 3),
+                                        ("res2net50_w24_s4_c32", 40, 37, 2),
                                         ("res2net101_w24_s4_c32_att", 80, 64, 3)])
 def test_conv3_win_bitwise_pipe(weights, name, F, T, N, monkeypatch):
     """The window-staged 3x3 (input rows fetched once per tile into a

@@ -124,6 +124,10 @@ int gemm_pipe_ok(const ConvParams& p);
 hipError_t launch_gemm_pipe(const ConvParams& p, int num_cu, int variant, hipStream_t s);
 // Window-staged 3x3 (conv3w.hip) for the w = 96 stride-1 branches at image
 // width 20 or 10: same tiles / epilogue / bits as conv3x3_pipe.
+// Register-weight 3x3 (conv3r.hip): w = 96 stride-1 branches, weights in
+// registers, the input window staged once per 128-pixel tile.
+int conv3_rw_ok(const ConvParams& p);
+hipError_t launch_conv3_rw(const ConvParams& p, int num_cu, hipStream_t s);
 int conv3_win_ok(const ConvParams& p);
 hipError_t launch_conv3_win(const ConvParams& p, int num_cu, hipStream_t s);
 // Wide-tile variant (gemm_wide.hip): 256 x BN tiles, BN = 256 (Cout % 256 == 0)
