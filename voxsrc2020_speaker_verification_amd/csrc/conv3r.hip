@@ -41,7 +41,7 @@ constexpr int CR_NT = 64 * CR_NW;
 constexpr int CR_KS = 9 * CR_C / 32;   // 27 k-steps
 constexpr int CR_NCH = CR_C / 8;       // 12 chunks per pixel
 
-typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ void cr_glds16(const void* src, uint32_t lds) {
   unsigned keep;
@@ -57,8 +57,8 @@ __device__ __forceinline__ void cr_glds16(const void* src, uint32_t lds) {
 }
 // the trailing s_nop keeps the next instruction from overwriting the data
 // registers before the store has read them
-__device__ __forceinline__ void cr_st8(void* dst, u32x2 v) {
-  asm volatile("global_store_dwordx2 %0, %1, off\n\ts_nop 1" : : "v"(dst), "v"(v) : "memory");
+__device__ __forceinline__ void cr_st16(void* dst, u32x4 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" : : "v"(dst), "v"(v) : "memory");
 }
 #define CR_W(n) \
   case n: asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory"); break;
@@ -88,11 +88,13 @@ struct CrCfg {
   static constexpr int XPC = XZB / 1024;
   static constexpr int PCS = WPC + XPC;                           // pieces per tile
   static constexpr int BUF = PCS * 1024;                          // one buffer: window | xz
-  static constexpr int LDS = 2 * BUF + 2 * CR_C * 4;
+  static constexpr int YST = 13 * 16;                             // staged y: pixel stride (odd units)
+  static constexpr int YSB = CR_TP * YST;
+  static constexpr int LDS = 2 * BUF + YSB + 2 * CR_C * 4;
   static constexpr int PPW = (PCS + CR_NW - 1) / CR_NW;           // pieces per wave (max)
   static_assert(XZB % 1024 == 0, "xz pieces");
   static_assert(LDS <= 163840, "LDS");
-  static_assert(PPW + 8 <= 16, "vmcnt table");
+  static_assert(CR_TP * CR_NCH % CR_NT == 0, "epilogue chunks");
 };
 
 #pragma clang fp contract(off)
@@ -134,7 +136,8 @@ __global__ __launch_bounds__(CR_NT) void conv3x3_rw(ConvParams p) {
   bf16_t* __restrict__ Z = reinterpret_cast<bf16_t*>(p.y2);
   const bf16_t* zero = reinterpret_cast<const bf16_t*>(g_cr_zero);
   const uint32_t lds0 = (uint32_t)(uintptr_t)smem;
-  float* bnm = reinterpret_cast<float*>(smem + 2 * K::BUF);
+  char* ys = smem + 2 * K::BUF;   // y of the tile, pixel-major, for row-contiguous stores
+  float* bnm = reinterpret_cast<float*>(smem + 2 * K::BUF + K::YSB);
   float* bni = bnm + CR_C;
   for (int c = tid; c < CR_C; c += CR_NT) {
     bnm[c] = p.mean[c];
@@ -239,23 +242,32 @@ __global__ __launch_bounds__(CR_NT) void conv3x3_rw(ConvParams p) {
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) {
       const int px = 16 * (4 * ph + jj) + col;
-      const bool in = p0 + px < HW;
-      const size_t pix = (size_t)n * HW + p0 + px;
       bf16x4 y;
 #pragma unroll
       for (int e = 0; e < 4; ++e) y[e] = (bf16_t)((acc[jj][e] - m[e]) * iv[e]);
       y = relu_bf16(y);
-      cr_st8((in && !(DBG & 8)) ? (void*)(Y + pix * p.ldy + co) : (void*)&g_cr_sink[lane], __builtin_bit_cast(u32x2, y));
-      if (HAS_Z) {
-        const bf16x4 xv = *reinterpret_cast<const bf16x4*>(xzl + px * (CR_C * 2) + co * 2);
-        bf16x4 zv;
+      *reinterpret_cast<bf16x4*>(ys + px * K::YST + co * 2) = y;
+    }
+    __syncthreads();
+    // every thread: 16-B chunks u of pixels px (192 contiguous bytes per pixel)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) zv[e] = (bf16_t)((float)xv[e] + (float)y[e]);
-        cr_st8((in && !(DBG & 8)) ? (void*)(Z + pix * p.ldy2 + co) : (void*)&g_cr_sink[lane], __builtin_bit_cast(u32x2, zv));
+    for (int i = 0; i < CR_TP * CR_NCH / CR_NT; ++i) {
+      const int c = tid + CR_NT * i;
+      const int px = c / CR_NCH, u = c - px * CR_NCH;
+      const bool in = p0 + px < HW && !(DBG & 8);
+      const size_t pix = (size_t)n * HW + p0 + px;
+      const bf16x8 y = *reinterpret_cast<const bf16x8*>(ys + px * K::YST + u * 16);
+      cr_st16(in ? (void*)(Y + pix * p.ldy + u * 8) : (void*)&g_cr_sink[lane], __builtin_bit_cast(u32x4, y));
+      if (HAS_Z) {
+        const bf16x8 xv = *reinterpret_cast<const bf16x8*>(xzl + px * (CR_C * 2) + u * 16);
+        bf16x8 zv;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) zv[e] = (bf16_t)((float)xv[e] + (float)y[e]);
+        cr_st16(in ? (void*)(Z + pix * p.ldy2 + u * 8) : (void*)&g_cr_sink[lane], __builtin_bit_cast(u32x4, zv));
       }
     }
     // the next tile's pieces (older than this epilogue's stores) have landed
-    if (tj + 1 < ntiles) cr_wait_vm(HAS_Z ? 8 : 4);
+    if (tj + 1 < ntiles) cr_wait_vm((HAS_Z ? 2 : 1) * (CR_TP * CR_NCH / CR_NT));
     __syncthreads();
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -265,7 +277,7 @@ int conv3_rw_ok(const ConvParams& p) {
   if (p.Cin != CR_C || p.Cout != CR_C || p.kh != 3 || p.kw != 3 || p.groups != 1) return 0;
   if (p.sh != 1 || p.sw != 1 || p.dh != 1 || p.dw != 1 || p.ph != 1 || p.pw != 1) return 0;
   if (p.Ho != p.H || p.Wo != p.W || !(p.W == 20 || p.W == 10)) return 0;
-  if (p.ldx % 8 || p.ldy % 4 || p.ldr % 8 || p.ldy2 % 4) return 0;
+  if (p.ldx % 8 || p.ldy % 8 || p.ldr % 8 || p.ldy2 % 8) return 0;
   if (p.flags != (EPI_AFFINE | EPI_RELU) || p.in_mean || p.x2 || !p.mean || !p.inv) return 0;
   if (p.y2 && p.y2 != p.res) return 0;   // z_{k+1} in place over x_{k+1}
   return p.N * p.H * p.W > 0;
