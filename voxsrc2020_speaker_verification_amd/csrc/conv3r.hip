@@ -87,10 +87,10 @@ struct CrCfg {
   static constexpr int XZB = CR_TP * CR_C * 2;                    // x_{k+1} rows of the tile
   static constexpr int XPC = XZB / 1024;
   static constexpr int PCS = WPC + XPC;                           // pieces per tile
-  static constexpr int BUF = PCS * 1024;                          // one buffer: window | xz
+  static constexpr int BUF = WPC * 1024;                          // one window buffer
   static constexpr int YST = 13 * 16;                             // staged y: pixel stride (odd units)
   static constexpr int YSB = CR_TP * YST;
-  static constexpr int LDS = 2 * BUF + YSB + 2 * CR_C * 4;
+  static constexpr int LDS = 2 * BUF + 2 * XZB + YSB + 2 * CR_C * 4;
   static constexpr int PPW = (PCS + CR_NW - 1) / CR_NW;           // pieces per wave (max)
   static_assert(XZB % 1024 == 0, "xz pieces");
   static_assert(LDS <= 163840, "LDS");
@@ -99,7 +99,8 @@ struct CrCfg {
 
 #pragma clang fp contract(off)
 // DBG (diagnostics, VOXEMB_CONV3_RW_DBG; garbage out): 1 = contiguous window
-// sources, 2 = no window DMA, 4 = no MFMA, 8 = no stores
+// sources, 2 = no window DMA, 4 = no MFMA, 8 = no stores, 16 = no k-loop,
+// 32 = no DMA waits
 template <int W, bool HAS_Z, int DBG = 0>
 __global__ __launch_bounds__(CR_NT) void conv3x3_rw(ConvParams p) {
   using K = CrCfg<W>;
@@ -136,8 +137,9 @@ __global__ __launch_bounds__(CR_NT) void conv3x3_rw(ConvParams p) {
   bf16_t* __restrict__ Z = reinterpret_cast<bf16_t*>(p.y2);
   const bf16_t* zero = reinterpret_cast<const bf16_t*>(g_cr_zero);
   const uint32_t lds0 = (uint32_t)(uintptr_t)smem;
-  char* ys = smem + 2 * K::BUF;   // y of the tile, pixel-major, for row-contiguous stores
-  float* bnm = reinterpret_cast<float*>(smem + 2 * K::BUF + K::YSB);
+  char* xzb = smem + 2 * K::BUF;  // x_{k+1} rows of a tile, double-buffered
+  char* ys = xzb + 2 * K::XZB;    // y of a tile, pixel-major, for row-contiguous stores
+  float* bnm = reinterpret_cast<float*>(ys + K::YSB);
   float* bni = bnm + CR_C;
   for (int c = tid; c < CR_C; c += CR_NT) {
     bnm[c] = p.mean[c];
@@ -178,78 +180,40 @@ __global__ __launch_bounds__(CR_NT) void conv3x3_rw(ConvParams p) {
       src = XZ + ((size_t)n * HW + pix) * p.ldr + c * 8;
     }
     if ((DBG & 2) && q < K::WPC) return;
-    cr_glds16(src, lds0 + (uint32_t)b * K::BUF + (uint32_t)q * 1024u);
+    const uint32_t dst = q < K::WPC ? lds0 + (uint32_t)b * K::BUF + (uint32_t)q * 1024u
+                                    : lds0 + 2u * K::BUF + (uint32_t)b * K::XZB +
+                                          (uint32_t)(q - K::WPC) * 1024u;
+    cr_glds16(src, dst);
   };
-  // this wave's pieces of a tile: q = wave, wave + 12, ...
-  auto issue_tile = [&](int tj, int b) __attribute__((always_inline)) {
+  // this wave's window pieces of a tile (q = wave, wave + 12, ...) and its
+  // x_{k+1} pieces; returns the count issued (wave-uniform)
+  auto issue_win = [&](int tj, int b) __attribute__((always_inline)) {
+    int c = 0;
 #pragma unroll
-    for (int i = 0; i < K::PPW; ++i) {
+    for (int i = 0; i < (K::WPC + CR_NW - 1) / CR_NW; ++i) {
       const int q = wave + CR_NW * i;
-      if (q < K::PCS && (HAS_Z || q < K::WPC)) issue_piece(tj, q, b);
+      if (q < K::WPC) {
+        issue_piece(tj, q, b);
+        ++c;
+      }
+    }
+    return c;
+  };
+  auto issue_xz = [&](int tj, int b) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < (K::XPC + CR_NW - 1) / CR_NW; ++i) {
+      const int q = K::WPC + wave + CR_NW * i;
+      if (HAS_Z && q < K::PCS) issue_piece(tj, q, b);
     }
   };
-
-  issue_tile(0, 0);
-  cr_wait_vm(0);
-  __syncthreads();
-
-  // chunk c = 4 part + g of a k-step lives in sub-plane 2 part + g/2, parity g%2
-  int cg[3];
-#pragma unroll
-  for (int part = 0; part < 3; ++part) cg[part] = ((2 * part + (g >> 1)) * SPW + (g & 1)) * 16;
-
-  for (int tj = 0; tj < ntiles; ++tj) {
-    const int b = tj & 1;
-    if (tj + 1 < ntiles) issue_tile(tj + 1, b ^ 1);
+  // store pass of tile tj (deferred into the next tile, so its HBM writes
+  // drain under MFMAs): y from the staging, z = x_{k+1} + y, 16-B chunks u of
+  // pixels px (192 contiguous bytes per pixel)
+  auto store_pass = [&](int tj) __attribute__((always_inline)) {
     const int id = t_first + tj * t_step;
     const int n = id / tpu, t = id - n * tpu;
     const int p0 = t * CR_TP;
-    const char* win = smem + b * K::BUF;   // this tile's window | xz
-    // per pixel tile: byte address of the (ky, kx) = (0, 0) tap slot of the
-    // lane's pixel; + cg[part] + 32 (ky SW + kx) per k-step
-    int bj[4];
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      const int pc = min(p0 + 16 * (4 * ph + jj) + col, HW - 1);
-      const int prow = pc / W - (p0 / W - 1);   // window row of the pixel (>= 1)
-      bj[jj] = b * K::BUF + 32 * ((prow - 1) * SW + (pc % W));
-    }
-    f32x4 acc[4];
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) acc[jj] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < CR_KS; ++s) {
-      const int tap = s / 3, part = s % 3;
-      const int off = 32 * ((tap / 3) * SW + tap % 3);
-      bf16x8 bf[4];
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        int a = bj[jj] + cg[part];
-        asm volatile("" : "+v"(a));   // one add per read, nothing precomputed per k-step
-        bf[jj] = *reinterpret_cast<const bf16x8*>(smem + a + off);
-      }
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj)
-        if (!(DBG & 4)) acc[jj] = mfma_step(wr[s], bf[jj], acc[jj]);
-        else acc[jj][0] += (float)bf[jj][0];
-      __builtin_amdgcn_sched_barrier(0);   // fragments of one k-step live at a time
-    }
-    // epilogue: 4 output channels 16 ct + 4 g of pixel 16 j + col
-    const int co = 16 * ct + 4 * g;
-    const f32x4 m = *reinterpret_cast<const f32x4*>(bnm + co);
-    const f32x4 iv = *reinterpret_cast<const f32x4*>(bni + co);
-    const char* xzl = win + K::WPC * 1024;
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      const int px = 16 * (4 * ph + jj) + col;
-      bf16x4 y;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) y[e] = (bf16_t)((acc[jj][e] - m[e]) * iv[e]);
-      y = relu_bf16(y);
-      *reinterpret_cast<bf16x4*>(ys + px * K::YST + co * 2) = y;
-    }
-    __syncthreads();
-    // every thread: 16-B chunks u of pixels px (192 contiguous bytes per pixel)
+    const char* xzl = xzb + (tj & 1) * K::XZB;
 #pragma unroll
     for (int i = 0; i < CR_TP * CR_NCH / CR_NT; ++i) {
       const int c = tid + CR_NT * i;
@@ -266,10 +230,75 @@ __global__ __launch_bounds__(CR_NT) void conv3x3_rw(ConvParams p) {
         cr_st16(in ? (void*)(Z + pix * p.ldy2 + u * 8) : (void*)&g_cr_sink[lane], __builtin_bit_cast(u32x4, zv));
       }
     }
-    // the next tile's pieces (older than this epilogue's stores) have landed
-    if (tj + 1 < ntiles) cr_wait_vm((HAS_Z ? 2 : 1) * (CR_TP * CR_NCH / CR_NT));
+  };
+
+  issue_win(0, 0);
+  cr_wait_vm(0);
+  __syncthreads();
+
+  // chunk c = 4 part + g of a k-step lives in sub-plane 2 part + g/2, parity g%2
+  int cg[3];
+#pragma unroll
+  for (int part = 0; part < 3; ++part) cg[part] = ((2 * part + (g >> 1)) * SPW + (g & 1)) * 16;
+
+  // tile tj: [pass: stores of tile tj-1] [DMA: window tj+1, x rows tj] [27
+  // k-steps] | barrier | [y of tile tj -> staging] [DMA landed] | barrier
+  for (int tj = 0; tj < ntiles; ++tj) {
+    const int b = tj & 1;
+    if (tj > 0) store_pass(tj - 1);
+    if (tj + 1 < ntiles) issue_win(tj + 1, b ^ 1);
+    issue_xz(tj, b);
+    const int id = t_first + tj * t_step;
+    const int n = id / tpu, t = id - n * tpu;
+    const int p0 = t * CR_TP;
+    // per pixel tile: byte address of the (ky, kx) = (0, 0) tap slot of the
+    // lane's pixel; + cg[part] + 32 (ky SW + kx) per k-step
+    int bj[4];
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int pc = min(p0 + 16 * (4 * ph + jj) + col, HW - 1);
+      const int prow = pc / W - (p0 / W - 1);   // window row of the pixel (>= 1)
+      bj[jj] = b * K::BUF + 32 * ((prow - 1) * SW + (pc % W));
+    }
+    f32x4 acc[4];
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) acc[jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < ((DBG & 16) ? 0 : CR_KS); ++s) {
+      const int tap = s / 3, part = s % 3;
+      const int off = 32 * ((tap / 3) * SW + tap % 3);
+      bf16x8 bf[4];
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        int a = bj[jj] + cg[part];
+        asm volatile("" : "+v"(a));   // one add per read, nothing precomputed per k-step
+        bf[jj] = *reinterpret_cast<const bf16x8*>(smem + a + off);
+      }
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj)
+        if (!(DBG & 4)) acc[jj] = mfma_step(wr[s], bf[jj], acc[jj]);
+        else acc[jj][0] += (float)bf[jj][0];
+      __builtin_amdgcn_sched_barrier(0);   // fragments of one k-step live at a time
+    }
+    __syncthreads();   // every thread is done with the staging (store pass tj-1)
+    // y of tile tj: 4 output channels 16 ct + 4 g of pixel 16 j + col
+    const int co = 16 * ct + 4 * g;
+    const f32x4 m = *reinterpret_cast<const f32x4*>(bnm + co);
+    const f32x4 iv = *reinterpret_cast<const f32x4*>(bni + co);
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int px = 16 * (4 * ph + jj) + col;
+      bf16x4 y;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) y[e] = (bf16_t)((acc[jj][e] - m[e]) * iv[e]);
+      y = relu_bf16(y);
+      *reinterpret_cast<bf16x4*>(ys + px * K::YST + co * 2) = y;
+    }
+    // window tj+1 and x rows tj have landed (the older stores have too)
+    if (!(DBG & 32)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
+  store_pass(ntiles - 1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
@@ -291,7 +320,7 @@ static void launch_cr(const ConvParams& p, int G, hipStream_t s) {
   }();
   switch (dbg) {
 #define CR_L(d) case d: hipLaunchKernelGGL((conv3x3_rw<W, Z, d>), dim3(G), dim3(CR_NT), CrCfg<W>::LDS, s, p); break;
-    CR_L(1) CR_L(2) CR_L(4) CR_L(8) CR_L(12) CR_L(6)
+    CR_L(1) CR_L(2) CR_L(8) CR_L(16) CR_L(32) CR_L(24) CR_L(48) CR_L(40)
 #undef CR_L
     default: hipLaunchKernelGGL((conv3x3_rw<W, Z, 0>), dim3(G), dim3(CR_NT), CrCfg<W>::LDS, s, p); break;
   }
