@@ -63,6 +63,9 @@ __device__ __forceinline__ void gw_glds16(const void* src, uint32_t lds) {
 __device__ __forceinline__ void gw_st16(void* dst, u32x4 v) {
   asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" : : "v"(dst), "v"(v) : "memory");
 }
+__device__ __forceinline__ void gw_st16_nt(void* dst, u32x4 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off nt\n\ts_nop 1" : : "v"(dst), "v"(v) : "memory");
+}
 
 #define GW_W(n) \
   case n: asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory"); break;
@@ -86,7 +89,8 @@ __device__ uint4 g_gw_sink[64];   // destination of masked lanes' stores
 
 #pragma clang fp contract(off)
 // DBG (diagnostics only, VOXEMB_GEMM_VAR): 1 = no MFMA / fragment reads,
-// 2 = no operand DMA, 4 = no output stores; results are garbage
+// 2 = no operand DMA, 4 = no output stores, 32 = non-temporal stores (same
+// results), 64 = every store to one sink line; results are garbage
 template <int BN, bool RES, int DBG = 0>
 __global__ __launch_bounds__(GW_NT) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void gemm1x1_wide(ConvParams p) {
@@ -268,7 +272,9 @@ void gemm1x1_wide(ConvParams p) {
                             : (void*)(Y2 + (size_t)pix * p.ldy2 + (ch - p.ysplit));
       else
         dst = &g_gw_sink[lane];
-      if (!(DBG & 4)) gw_st16(dst, __builtin_bit_cast(u32x4, o));
+      if (DBG & 64) dst = &g_gw_sink[lane];
+      if (DBG & 32) gw_st16_nt(dst, __builtin_bit_cast(u32x4, o));
+      else if (!(DBG & 4)) gw_st16(dst, __builtin_bit_cast(u32x4, o));
     }
   };
 
@@ -379,6 +385,8 @@ hipError_t launch_gemm_wide(const ConvParams& p0, int num_cu, int variant, hipSt
     case 14: launch_wide_t<4>(p, bn, G, lds, s); break;
     case 13: launch_wide_t<3>(p, bn, G, lds, s); break;
     case 16: launch_wide_t<6>(p, bn, G, lds, s); break;
+    case 42: launch_wide_t<32>(p, bn, G, lds, s); break;
+    case 74: launch_wide_t<64>(p, bn, G, lds, s); break;
     case 15: launch_wide_t<5>(p, bn, G, lds, s); break;
     default: launch_wide_t<0>(p, bn, G, lds, s); break;
   }
