@@ -414,24 +414,30 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
           *reinterpret_cast<bf16x4*>(rings + zsl + pxo) = inimg ? add4(x, y) : bf16x4{};
         }
       };
-      for (int j = 0; j < PT; j += 2) {
-        const bool two = j + 1 < PT;
-        const int px0 = 16 * j + col, px1 = px0 + 16;
-        bf16x8 b0[KST], b1[KST];
+      // the PT pixel tiles as independent accumulators, fragments read one
+      // k-step ahead (same K order per tile)
+      f32x4 acc[PT];
+      bf16x8 bc[PT], bn[PT];
 #pragma unroll
-        for (int s = 0; s < KST; ++s) {
-          b0[s] = *reinterpret_cast<const bf16x8*>(zring + boff[s] + 16 * j * ASTR);
-          b1[s] = two ? *reinterpret_cast<const bf16x8*>(zring + boff[s] + 16 * (j + 1) * ASTR) : bf16x8{};
-        }
-        f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s = 0; s < KST; ++s) {
-          acc0 = mfma_step(wb[s], b0[s], acc0);
-          acc1 = mfma_step(wb[s], b1[s], acc1);
-        }
-        epilogue(acc0, px0);
-        if (two) epilogue(acc1, px1);
+      for (int j = 0; j < PT; ++j) {
+        acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        bc[j] = *reinterpret_cast<const bf16x8*>(zring + boff[0] + 16 * j * ASTR);
       }
+#pragma unroll
+      for (int s = 0; s < KST; ++s) {
+        if (s + 1 < KST) {
+#pragma unroll
+          for (int j = 0; j < PT; ++j)
+            bn[j] = *reinterpret_cast<const bf16x8*>(zring + boff[s + 1] + 16 * j * ASTR);
+        }
+#pragma unroll
+        for (int j = 0; j < PT; ++j) acc[j] = mfma_step(wb[s], bc[j], acc[j]);
+#pragma unroll
+        for (int j = 0; j < PT; ++j) bc[j] = bn[j];
+        __builtin_amdgcn_sched_barrier(0);   // reads stay one k-step ahead
+      }
+#pragma unroll
+      for (int j = 0; j < PT; ++j) epilogue(acc[j], 16 * j + col);
     }
     __syncthreads();
   };
