@@ -336,7 +336,12 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
           o[4 + e] = (bf16_t)v1;
         }
         o = relu_bf16(o);
-        if (px < W) *reinterpret_cast<bf16x8*>(Y + (img + (size_t)c * W + px) * C + ch) = o;
+        if (q.dbg & 16) {   // diagnostics: no output stores / all to one line
+        } else if (q.dbg & 32) {
+          if (px < W) *reinterpret_cast<bf16x8*>(Y + lane * 8) = o;
+        } else if (px < W) {
+          *reinterpret_cast<bf16x8*>(Y + (img + (size_t)c * W + px) * C + ch) = o;
+        }
       };
 #pragma unroll
       for (int j = 0; j < PT; j += 2) {
