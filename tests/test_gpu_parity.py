@@ -248,6 +248,27 @@ def test_gemm_pipe_bitwise_many_tiles(weights, N, T, monkeypatch):
 
 @pytest.mark.parametrize("name,F,T,N", [("res2net50_w24_s4_c32", 80, 200, 16),
                                         ("res2net50_w24_s4_c32", 80, 123, 7),
+                                        ("res2net50_w24_s4_c32", 40, 75, 3),
+                                        ("res2net101_w24_s4_c32_att", 80, 64, 3)])
+@pytest.mark.parametrize("var", ["1", "-1"])
+def test_gemm_ws_bitwise_wide(weights, name, F, T, N, var, monkeypatch):
+    """The wave-specialised GEMM (4 loader waves own the operand DMA, 8 compute
+    waves never wait on it; default for the 192-wide tiles, forced for every
+    shape with VOXEMB_GEMM_VAR=1, off with -1) gives the same bits."""
+    from voxsrc2020_speaker_verification_amd import synth
+    spec, t, blob = weights(name, F)
+    x = synth.make_features(N, T, F, seed=43)
+    monkeypatch.setenv("VOXEMB_GEMM_VAR", var)
+    with _extractor(blob, "bf16") as ex:
+        got = ex.run(x)
+    monkeypatch.setenv("VOXEMB_NO_GEMM_WIDE", "1")
+    with _extractor(blob, "bf16") as ex:
+        ref = ex.run(x)
+    assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("name,F,T,N", [("res2net50_w24_s4_c32", 80, 200, 16),
+                                        ("res2net50_w24_s4_c32", 80, 123, 7),
                                         ("res2net50_w24_s4_c64", 40, 75, 3),
                                         ("res2net101_w24_s4_c32_att", 80, 64, 3),
                                         ("tdnn", 80, 200, 40)])

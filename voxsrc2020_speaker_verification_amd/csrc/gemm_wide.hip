@@ -346,6 +346,249 @@ void gemm1x1_wide(ConvParams p) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// ----------------------------------------------------------------------------
+// Wave-specialised variant: the same tiles, ring, K order and epilogue, with
+// the operand DMA moved to 4 loader waves (waves 8..11) so the 8 compute waves
+// never issue or wait on a global_load_lds.  In gemm1x1_wide every wave issues
+// its share of a K-step's DMA and then runs its MFMAs, and on these L2-fed
+// streams the two add (DESIGN.md "What bounds the DMA-fed kernels"); here a
+// loader wave only waits for its own pieces before the step's barrier.
+// 12 waves (3 per SIMD) cap the VGPRs at 168.  Bitwise equal to gemm1x1_wide.
+constexpr int GS_NT = 768;
+constexpr int GS_NL = 4;   // loader waves
+
+template <int BN, bool RES>
+__global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
+  constexpr int NI = BN / 32;
+  constexpr int NQ = NI / 2;
+  constexpr int GRP = (BN + GW_BM) / 16;     // 1-KB DMA groups per operand step
+  constexpr int NLL = GRP / GS_NL;           // per loader wave
+  constexpr int NR = RES ? GW_NR : 0;
+  static_assert(GRP % GS_NL == 0, "groups per loader");
+  static_assert(!RES || GRP == 32, "residual phases: 32 groups");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool loader = wave >= 8;
+  const int lw = wave - 8;
+  const int wm = (wave >> 2) & 1, wn = wave & 3;
+  const int col = lane & 15, g = lane >> 4;
+  const int M = p.N * p.Ho * p.Wo;
+  const int HoWo = p.Ho * p.Wo;
+  const int KT = p.kp / 32;
+  const int SPT = KT + NR;
+  const int cblocks = p.coutp / BN;
+  const int T = ((M + GW_BM - 1) / GW_BM) * cblocks;
+  int t_first, t_step, ntiles;
+  {
+    const int G = gridDim.x;
+    if ((G & 7) == 0) {
+      const int x = blockIdx.x & 7, bi = blockIdx.x >> 3, nb = G >> 3;
+      const int b0 = (int)((long)x * T / 8), b1 = (int)((long)(x + 1) * T / 8);
+      t_first = b0 + bi;
+      t_step = nb;
+      ntiles = t_first < b1 ? (b1 - t_first + nb - 1) / nb : 0;
+    } else {
+      t_first = blockIdx.x;
+      t_step = G;
+      ntiles = t_first < T ? (T - t_first + G - 1) / G : 0;
+    }
+  }
+  if (ntiles == 0) return;
+  const int S = ntiles * SPT;
+
+  const bf16_t* __restrict__ X = reinterpret_cast<const bf16_t*>(p.x);
+  const bf16_t* __restrict__ Wt = reinterpret_cast<const bf16_t*>(p.w);
+  const bf16_t* __restrict__ R = reinterpret_cast<const bf16_t*>(p.res);
+  bf16_t* __restrict__ Y = reinterpret_cast<bf16_t*>(p.y);
+  bf16_t* __restrict__ Y2 = reinterpret_cast<bf16_t*>(p.y2);
+  const int flags = p.flags;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)smem;
+
+  float* tab = reinterpret_cast<float*>(smem + GW_NST * GW_SLOT);
+  if (flags & EPI_AFFINE) {
+    for (int k = tid; k < p.coutp; k += GS_NT) {
+      tab[k] = k < p.Cout ? p.mean[k] : 0.f;
+      tab[p.coutp + k] = k < p.Cout ? p.inv[k] : 0.f;
+    }
+  }
+  __syncthreads();
+
+  if (loader) {
+    // ---- loader waves: groups gi = lw + 4 i of every step
+    const bf16_t* src[NLL];
+    int l_tile = 0, l_k = 0, l_co0 = 0, l_px0 = 0;
+    auto set_load_tile = [&](int tj) {
+      const int lid = t_first + tj * t_step;
+      l_co0 = (lid % cblocks) * BN;
+      l_px0 = (lid / cblocks) * GW_BM;
+#pragma unroll
+      for (int i = 0; i < NLL; ++i) {
+        const int gi = lw + GS_NL * i;
+        const int row = 16 * gi + (lane >> 2);
+        const int c = (lane & 3) ^ gw_swz(row);
+        if (row < BN) {
+          src[i] = Wt + (size_t)(l_co0 + row) * p.kp + c * 8;
+        } else {
+          const int pix = min(l_px0 + row - BN, M - 1);
+          const int n = pix / HoWo, rr = pix - n * HoWo;
+          const int ho = rr / p.Wo, wo = rr - ho * p.Wo;
+          src[i] = X + (((size_t)n * p.H + ho * p.sh) * p.W + wo * p.sw) * p.ldx + c * 8;
+        }
+      }
+    };
+    auto issue = [&](int slot) {
+#pragma unroll
+      for (int i = 0; i < NLL; ++i) {
+        const int gi = lw + GS_NL * i;
+        const uint32_t base = lds0 + (uint32_t)slot * GW_SLOT + (uint32_t)gi * 1024u;
+        if (l_k < KT) {
+          gw_glds16(src[i] + l_k * 32, base);
+        } else if (RES) {
+          // residual phase ph: slot row r (512 B) = pixel l_px0 + 64 (gi / 8) + 16 ph + r % 16
+          const int ph = l_k - KT;
+          const int row = 2 * gi + (lane >> 5);
+          const int c = (lane & 31) ^ (row & 15);
+          const int pix = min(l_px0 + 64 * (gi >> 3) + 16 * ph + (row & 15), M - 1);
+          gw_glds16(R + (size_t)pix * p.ldr + l_co0 + c * 8, base);
+        }
+      }
+      if (l_k + 1 < SPT) {
+        ++l_k;
+      } else if (l_tile + 1 < ntiles) {
+        ++l_tile;
+        l_k = 0;
+        set_load_tile(l_tile);
+      }
+    };
+    set_load_tile(0);
+    issue(0);
+    issue(1);
+    issue(2);
+    for (int s = 0; s < S; ++s) {
+      gw_wait_vm(2 * NLL);   // step s landed; steps s+1, s+2 in flight
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      issue((s + 3) & 3);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    return;
+  }
+
+  // ---- compute waves (2 cout halves x 4 pixel quarters), as gemm1x1_wide
+  f32x4 acc[NI][4];
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int cs = (g ^ gw_swz(col)) << 4;
+  const int offa = (wm * (BN / 2) + col) * 64 + cs;
+  const int offb = (BN + wn * 64 + col) * 64 + cs;
+
+  auto epi = [&](auto jc, int co0, int px0, const char* rl) {
+    constexpr int J = decltype(jc)::value;
+    const int pix = px0 + wn * 64 + 16 * J + col;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int chl = wm * (BN / 2) + 32 * q + 8 * g;
+      const int ch = co0 + chl;
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = acc[2 * q][J][e];
+        v[4 + e] = acc[2 * q + 1][J][e];
+      }
+      if (flags & EPI_PRE_RELU) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+      }
+      if (flags & EPI_AFFINE) {
+        // BN values re-read per column: not kept live across the 4 columns
+        int tch = ch;
+        asm volatile("" : "+v"(tch));
+        const f32x4 m0 = *reinterpret_cast<const f32x4*>(tab + tch);
+        const f32x4 m1 = *reinterpret_cast<const f32x4*>(tab + tch + 4);
+        const f32x4 i0 = *reinterpret_cast<const f32x4*>(tab + p.coutp + tch);
+        const f32x4 i1 = *reinterpret_cast<const f32x4*>(tab + p.coutp + tch + 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = (v[e] - m0[e]) * i0[e];
+          v[4 + e] = (v[4 + e] - m1[e]) * i1[e];
+        }
+      }
+      if (RES && rl && ch < p.ysplit) {
+        const int row = wn * 16 + col;
+        const bf16x8 r8 = *reinterpret_cast<const bf16x8*>(
+            rl + row * 512 + ((((chl >> 3) ^ (row & 15))) << 4));
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += (float)r8[e];
+      }
+      if (flags & EPI_RELU) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+      }
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = (bf16_t)v[e];
+      void* dst;
+      if (ch < p.Cout && pix < M)
+        dst = ch < p.ysplit ? (void*)(Y + (size_t)pix * p.ldy + ch)
+                            : (void*)(Y2 + (size_t)pix * p.ldy2 + (ch - p.ysplit));
+      else
+        dst = &g_gw_sink[lane];
+      gw_st16(dst, __builtin_bit_cast(u32x4, o));
+    }
+  };
+
+  int c_tile = 0, c_k = 0;
+  for (int s = 0; s < S; ++s) {
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    const int lid = t_first + c_tile * t_step;
+    const int co0 = (lid % cblocks) * BN;
+    const int px0 = (lid / cblocks) * GW_BM;
+    const char* L = smem + (s & 3) * GW_SLOT;
+    if (c_k < KT) {
+      // B fragments for the step, A fragments two cout blocks ahead (register budget)
+      bf16x8 a[NI], b[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const bf16x8*>(L + offb + j * 1024);
+      a[0] = *reinterpret_cast<const bf16x8*>(L + offa);
+      a[1] = *reinterpret_cast<const bf16x8*>(L + offa + 1024);
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        if (i + 2 < NI) a[i + 2] = *reinterpret_cast<const bf16x8*>(L + offa + (i + 2) * 1024);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma_step(a[i], b[j], acc[i][j]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (!RES && c_k == KT - 1) {
+        epi(std::integral_constant<int, 0>{}, co0, px0, nullptr);
+        epi(std::integral_constant<int, 1>{}, co0, px0, nullptr);
+        epi(std::integral_constant<int, 2>{}, co0, px0, nullptr);
+        epi(std::integral_constant<int, 3>{}, co0, px0, nullptr);
+      }
+    } else if (RES) {
+      const int ph = c_k - KT;
+      if (ph == 0) epi(std::integral_constant<int, 0>{}, co0, px0, L);
+      else if (ph == 1) epi(std::integral_constant<int, 1>{}, co0, px0, L);
+      else if (ph == 2) epi(std::integral_constant<int, 2>{}, co0, px0, L);
+      else epi(std::integral_constant<int, 3>{}, co0, px0, L);
+    }
+    if (c_k + 1 == SPT) {
+#pragma unroll
+      for (int i = 0; i < NI; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      c_k = 0;
+      ++c_tile;
+    } else {
+      ++c_k;
+    }
+  }
+}
+
 // BN of the wide tile for this conv, or 0 if gemm1x1_wide does not apply
 int gemm_wide_bn(const ConvParams& p) {
   if (p.in_mean || p.kp % 32 || p.kp / 32 < 3 || p.Cout % 8) return 0;
@@ -379,6 +622,20 @@ hipError_t launch_gemm_wide(const ConvParams& p0, int num_cu, int variant, hipSt
   int G = num_cu < T ? num_cu : T;
   G = G / 8 * 8;
   const size_t lds = GW_NST * GW_SLOT + ((p.flags & EPI_AFFINE) ? 8 * (size_t)p.coutp : 0);
+  // the 192-wide tiles run wave-specialised by default (10 % faster: their
+  // compute waves fit the 12-wave register cap); VOXEMB_GEMM_VAR=1 forces it
+  // for every shape, -1 disables it
+  if (variant == 0 && bn == 192) variant = 1;
+  if (variant == -1) variant = 0;
+  if (variant == 1) {   // wave-specialised
+    if (bn == 192)
+      hipLaunchKernelGGL((gemm1x1_ws<192, false>), dim3(G), dim3(GS_NT), lds, s, p);
+    else if (p.flags & EPI_RES)
+      hipLaunchKernelGGL((gemm1x1_ws<256, true>), dim3(G), dim3(GS_NT), lds, s, p);
+    else
+      hipLaunchKernelGGL((gemm1x1_ws<256, false>), dim3(G), dim3(GS_NT), lds, s, p);
+    return hipGetLastError();
+  }
   switch (variant) {   // 0 = the product kernel; 11..17 = diagnostics (DBG = variant - 10)
     case 11: launch_wide_t<1>(p, bn, G, lds, s); break;
     case 12: launch_wide_t<2>(p, bn, G, lds, s); break;
