@@ -253,8 +253,9 @@ def test_gemm_pipe_bitwise_many_tiles(weights, N, T, monkeypatch):
 @pytest.mark.parametrize("var", ["1", "-1"])
 def test_gemm_ws_bitwise_wide(weights, name, F, T, N, var, monkeypatch):
     """The wave-specialised GEMM (4 loader waves own the operand DMA, 8 compute
-    waves never wait on it; default for the 192-wide tiles, forced for every
-    shape with VOXEMB_GEMM_VAR=1, off with -1) gives the same bits."""
+    waves never wait on it; 192-pixel tiles for the 256-wide shapes; the
+    default, VOXEMB_GEMM_VAR=-1 selects gemm1x1_wide) gives the same bits as
+    gemm1x1_pipe."""
     from voxsrc2020_speaker_verification_amd import synth
     spec, t, blob = weights(name, F)
     x = synth.make_features(N, T, F, seed=43)

@@ -357,15 +357,19 @@ void gemm1x1_wide(ConvParams p) {
 constexpr int GS_NT = 768;
 constexpr int GS_NL = 4;   // loader waves
 
-template <int BN, bool RES>
+// BM = pixels per tile: 256, or 192 for the 256-wide tiles (their compute waves
+// then hold 96 accumulators and fit the cap; the residual takes 3 phases)
+template <int BN, bool RES, int BM = GW_BM>
 __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
   constexpr int NI = BN / 32;
   constexpr int NQ = NI / 2;
-  constexpr int GRP = (BN + GW_BM) / 16;     // 1-KB DMA groups per operand step
+  constexpr int NJ = BM / 64;                // 16-pixel columns per wave
+  constexpr int GRP = (BN + BM) / 16;        // 1-KB DMA groups per operand step
   constexpr int NLL = GRP / GS_NL;           // per loader wave
-  constexpr int NR = RES ? GW_NR : 0;
+  constexpr int NR = RES ? NJ : 0;           // residual phases (64 pixels x 256 couts each)
+  constexpr int NLR = 32 / GS_NL;            // residual pieces per loader wave
   static_assert(GRP % GS_NL == 0, "groups per loader");
-  static_assert(!RES || GRP == 32, "residual phases: 32 groups");
+  static_assert(!RES || BN == 256, "residual phases: 256 couts");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -379,7 +383,7 @@ __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
   const int KT = p.kp / 32;
   const int SPT = KT + NR;
   const int cblocks = p.coutp / BN;
-  const int T = ((M + GW_BM - 1) / GW_BM) * cblocks;
+  const int T = ((M + BM - 1) / BM) * cblocks;
   int t_first, t_step, ntiles;
   {
     const int G = gridDim.x;
@@ -422,7 +426,7 @@ __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
     auto set_load_tile = [&](int tj) {
       const int lid = t_first + tj * t_step;
       l_co0 = (lid % cblocks) * BN;
-      l_px0 = (lid / cblocks) * GW_BM;
+      l_px0 = (lid / cblocks) * BM;
 #pragma unroll
       for (int i = 0; i < NLL; ++i) {
         const int gi = lw + GS_NL * i;
@@ -438,21 +442,29 @@ __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
         }
       }
     };
-    auto issue = [&](int slot) {
+    // returns the pieces issued (an operand step NLL, a residual phase NLR)
+    auto issue = [&](int slot) -> int {
+      int n = 0;
+      if (l_k < KT) {
 #pragma unroll
-      for (int i = 0; i < NLL; ++i) {
-        const int gi = lw + GS_NL * i;
-        const uint32_t base = lds0 + (uint32_t)slot * GW_SLOT + (uint32_t)gi * 1024u;
-        if (l_k < KT) {
-          gw_glds16(src[i] + l_k * 32, base);
-        } else if (RES) {
-          // residual phase ph: slot row r (512 B) = pixel l_px0 + 64 (gi / 8) + 16 ph + r % 16
-          const int ph = l_k - KT;
+        for (int i = 0; i < NLL; ++i) {
+          const int gi = lw + GS_NL * i;
+          gw_glds16(src[i] + l_k * 32, lds0 + (uint32_t)slot * GW_SLOT + (uint32_t)gi * 1024u);
+        }
+        n = NLL;
+      } else if (RES) {
+        // residual phase ph: slot row r (512 B) = pixel l_px0 + (BM/4) (r / 16) + 16 ph + r % 16
+        const int ph = l_k - KT;
+#pragma unroll
+        for (int i = 0; i < NLR; ++i) {
+          const int gi = lw + GS_NL * i;
           const int row = 2 * gi + (lane >> 5);
           const int c = (lane & 31) ^ (row & 15);
-          const int pix = min(l_px0 + 64 * (gi >> 3) + 16 * ph + (row & 15), M - 1);
-          gw_glds16(R + (size_t)pix * p.ldr + l_co0 + c * 8, base);
+          const int pix = min(l_px0 + (BM / 4) * (gi >> 3) + 16 * ph + (row & 15), M - 1);
+          gw_glds16(R + (size_t)pix * p.ldr + l_co0 + c * 8,
+                    lds0 + (uint32_t)slot * GW_SLOT + (uint32_t)gi * 1024u);
         }
+        n = NLR;
       }
       if (l_k + 1 < SPT) {
         ++l_k;
@@ -461,34 +473,36 @@ __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
         l_k = 0;
         set_load_tile(l_tile);
       }
+      return n;
     };
     set_load_tile(0);
     issue(0);
-    issue(1);
-    issue(2);
+    int n1 = issue(1), n2 = issue(2);   // pieces of the two steps after the awaited one
     for (int s = 0; s < S; ++s) {
-      gw_wait_vm(2 * NLL);   // step s landed; steps s+1, s+2 in flight
+      gw_wait_vm(n1 + n2);   // step s landed; steps s+1, s+2 in flight
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
-      issue((s + 3) & 3);
+      const int n3 = issue((s + 3) & 3);
+      n1 = n2;
+      n2 = n3;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     return;
   }
 
   // ---- compute waves (2 cout halves x 4 pixel quarters), as gemm1x1_wide
-  f32x4 acc[NI][4];
+  f32x4 acc[NI][NJ];
 #pragma unroll
   for (int i = 0; i < NI; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int cs = (g ^ gw_swz(col)) << 4;
   const int offa = (wm * (BN / 2) + col) * 64 + cs;
-  const int offb = (BN + wn * 64 + col) * 64 + cs;
+  const int offb = (BN + wn * (BM / 4) + col) * 64 + cs;
 
   auto epi = [&](auto jc, int co0, int px0, const char* rl) {
     constexpr int J = decltype(jc)::value;
-    const int pix = px0 + wn * 64 + 16 * J + col;
+    const int pix = px0 + wn * (BM / 4) + 16 * J + col;
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const int chl = wm * (BN / 2) + 32 * q + 8 * g;
@@ -547,40 +561,40 @@ __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
     __builtin_amdgcn_sched_barrier(0);
     const int lid = t_first + c_tile * t_step;
     const int co0 = (lid % cblocks) * BN;
-    const int px0 = (lid / cblocks) * GW_BM;
+    const int px0 = (lid / cblocks) * BM;
     const char* L = smem + (s & 3) * GW_SLOT;
     if (c_k < KT) {
       // B fragments for the step, A fragments two cout blocks ahead (register budget)
-      bf16x8 a[NI], b[4];
+      bf16x8 a[NI], b[NJ];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const bf16x8*>(L + offb + j * 1024);
+      for (int j = 0; j < NJ; ++j) b[j] = *reinterpret_cast<const bf16x8*>(L + offb + j * 1024);
       a[0] = *reinterpret_cast<const bf16x8*>(L + offa);
       a[1] = *reinterpret_cast<const bf16x8*>(L + offa + 1024);
 #pragma unroll
       for (int i = 0; i < NI; ++i) {
         if (i + 2 < NI) a[i + 2] = *reinterpret_cast<const bf16x8*>(L + offa + (i + 2) * 1024);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mfma_step(a[i], b[j], acc[i][j]);
+        for (int j = 0; j < NJ; ++j) acc[i][j] = mfma_step(a[i], b[j], acc[i][j]);
         __builtin_amdgcn_sched_barrier(0);
       }
       if (!RES && c_k == KT - 1) {
         epi(std::integral_constant<int, 0>{}, co0, px0, nullptr);
         epi(std::integral_constant<int, 1>{}, co0, px0, nullptr);
         epi(std::integral_constant<int, 2>{}, co0, px0, nullptr);
-        epi(std::integral_constant<int, 3>{}, co0, px0, nullptr);
+        if constexpr (NJ > 3) epi(std::integral_constant<int, 3>{}, co0, px0, nullptr);
       }
     } else if (RES) {
       const int ph = c_k - KT;
       if (ph == 0) epi(std::integral_constant<int, 0>{}, co0, px0, L);
       else if (ph == 1) epi(std::integral_constant<int, 1>{}, co0, px0, L);
       else if (ph == 2) epi(std::integral_constant<int, 2>{}, co0, px0, L);
-      else epi(std::integral_constant<int, 3>{}, co0, px0, L);
+      else if constexpr (NJ > 3) epi(std::integral_constant<int, 3>{}, co0, px0, L);
     }
     if (c_k + 1 == SPT) {
 #pragma unroll
       for (int i = 0; i < NI; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
       c_k = 0;
       ++c_tile;
     } else {
@@ -622,18 +636,24 @@ hipError_t launch_gemm_wide(const ConvParams& p0, int num_cu, int variant, hipSt
   int G = num_cu < T ? num_cu : T;
   G = G / 8 * 8;
   const size_t lds = GW_NST * GW_SLOT + ((p.flags & EPI_AFFINE) ? 8 * (size_t)p.coutp : 0);
-  // the 192-wide tiles run wave-specialised by default (10 % faster: their
-  // compute waves fit the 12-wave register cap); VOXEMB_GEMM_VAR=1 forces it
-  // for every shape, -1 disables it
-  if (variant == 0 && bn == 192) variant = 1;
+  // wave-specialised by default (4-11 % faster per launch; the 256-wide tiles
+  // with 192 pixels so the compute waves fit the 12-wave register cap);
+  // VOXEMB_GEMM_VAR=-1 selects gemm1x1_wide
+  if (variant == 0) variant = 1;
   if (variant == -1) variant = 0;
   if (variant == 1) {   // wave-specialised
     if (bn == 192)
       hipLaunchKernelGGL((gemm1x1_ws<192, false>), dim3(G), dim3(GS_NT), lds, s, p);
-    else if (p.flags & EPI_RES)
-      hipLaunchKernelGGL((gemm1x1_ws<256, true>), dim3(G), dim3(GS_NT), lds, s, p);
-    else
-      hipLaunchKernelGGL((gemm1x1_ws<256, false>), dim3(G), dim3(GS_NT), lds, s, p);
+    else {
+      // 256-wide: 192-pixel tiles (their own tile count and grid)
+      const int T2 = ((M + 191) / 192) * (p.Cout / bn);
+      int G2 = num_cu < T2 ? num_cu : T2;
+      G2 = G2 >= 8 ? G2 / 8 * 8 : G2;
+      if (p.flags & EPI_RES)
+        hipLaunchKernelGGL((gemm1x1_ws<256, true, 192>), dim3(G2), dim3(GS_NT), lds, s, p);
+      else
+        hipLaunchKernelGGL((gemm1x1_ws<256, false, 192>), dim3(G2), dim3(GS_NT), lds, s, p);
+    }
     return hipGetLastError();
   }
   switch (variant) {   // 0 = the product kernel; 11..17 = diagnostics (DBG = variant - 10)
