@@ -359,7 +359,9 @@ constexpr int GS_NL = 4;   // loader waves
 
 // BM = pixels per tile: 256, or 192 for the 256-wide tiles (their compute waves
 // then hold 96 accumulators and fit the cap; the residual takes 3 phases)
-template <int BN, bool RES, int BM = GW_BM>
+// DBG (diagnostics, VOXEMB_GEMM_VAR 21/22): 1 = compute waves skip fragment
+// reads and MFMAs (stores kept), 2 = loaders issue no DMA; results garbage
+template <int BN, bool RES, int BM = GW_BM, int DBG = 0>
 __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
   constexpr int NI = BN / 32;
   constexpr int NQ = NI / 2;
@@ -430,8 +432,9 @@ __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
 #pragma unroll
       for (int i = 0; i < NLL; ++i) {
         const int gi = lw + GS_NL * i;
-        const int row = 16 * gi + (lane >> 2);
-        const int c = (lane & 3) ^ gw_swz(row);
+        // DBG 4 (timing only): 8 rows x 128 B per piece instead of 16 x 64 B
+        const int row = (DBG & 4) ? 16 * gi + 2 * (lane >> 3) : 16 * gi + (lane >> 2);
+        const int c = (DBG & 4) ? (lane & 7) : ((lane & 3) ^ gw_swz(row));
         if (row < BN) {
           src[i] = Wt + (size_t)(l_co0 + row) * p.kp + c * 8;
         } else {
@@ -449,9 +452,9 @@ __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
 #pragma unroll
         for (int i = 0; i < NLL; ++i) {
           const int gi = lw + GS_NL * i;
-          gw_glds16(src[i] + l_k * 32, lds0 + (uint32_t)slot * GW_SLOT + (uint32_t)gi * 1024u);
+          if (!(DBG & 2)) gw_glds16(src[i] + l_k * 32, lds0 + (uint32_t)slot * GW_SLOT + (uint32_t)gi * 1024u);
         }
-        n = NLL;
+        n = (DBG & 2) ? 0 : NLL;
       } else if (RES) {
         // residual phase ph: slot row r (512 B) = pixel l_px0 + (BM/4) (r / 16) + 16 ph + r % 16
         const int ph = l_k - KT;
@@ -461,10 +464,11 @@ __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
           const int row = 2 * gi + (lane >> 5);
           const int c = (lane & 31) ^ (row & 15);
           const int pix = min(l_px0 + (BM / 4) * (gi >> 3) + 16 * ph + (row & 15), M - 1);
-          gw_glds16(R + (size_t)pix * p.ldr + l_co0 + c * 8,
-                    lds0 + (uint32_t)slot * GW_SLOT + (uint32_t)gi * 1024u);
+          if (!(DBG & 2))
+            gw_glds16(R + (size_t)pix * p.ldr + l_co0 + c * 8,
+                      lds0 + (uint32_t)slot * GW_SLOT + (uint32_t)gi * 1024u);
         }
-        n = NLR;
+        n = (DBG & 2) ? 0 : NLR;
       }
       if (l_k + 1 < SPT) {
         ++l_k;
@@ -563,7 +567,14 @@ __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
     const int co0 = (lid % cblocks) * BN;
     const int px0 = (lid / cblocks) * BM;
     const char* L = smem + (s & 3) * GW_SLOT;
-    if (c_k < KT) {
+    if (c_k < KT && (DBG & 1)) {
+      if (!RES && c_k == KT - 1) {
+        epi(std::integral_constant<int, 0>{}, co0, px0, nullptr);
+        epi(std::integral_constant<int, 1>{}, co0, px0, nullptr);
+        epi(std::integral_constant<int, 2>{}, co0, px0, nullptr);
+        if constexpr (NJ > 3) epi(std::integral_constant<int, 3>{}, co0, px0, nullptr);
+      }
+    } else if (c_k < KT) {
       // B fragments for the step, A fragments two cout blocks ahead (register budget)
       bf16x8 a[NI], b[NJ];
 #pragma unroll
@@ -641,19 +652,27 @@ hipError_t launch_gemm_wide(const ConvParams& p0, int num_cu, int variant, hipSt
   // VOXEMB_GEMM_VAR=-1 selects gemm1x1_wide
   if (variant == 0) variant = 1;
   if (variant == -1) variant = 0;
-  if (variant == 1) {   // wave-specialised
-    if (bn == 192)
-      hipLaunchKernelGGL((gemm1x1_ws<192, false>), dim3(G), dim3(GS_NT), lds, s, p);
-    else {
-      // 256-wide: 192-pixel tiles (their own tile count and grid)
-      const int T2 = ((M + 191) / 192) * (p.Cout / bn);
-      int G2 = num_cu < T2 ? num_cu : T2;
-      G2 = G2 >= 8 ? G2 / 8 * 8 : G2;
-      if (p.flags & EPI_RES)
-        hipLaunchKernelGGL((gemm1x1_ws<256, true, 192>), dim3(G2), dim3(GS_NT), lds, s, p);
-      else
-        hipLaunchKernelGGL((gemm1x1_ws<256, false, 192>), dim3(G2), dim3(GS_NT), lds, s, p);
-    }
+  if (variant == 1 || (variant >= 21 && variant <= 25)) {   // wave-specialised
+    auto go = [&](auto dbgc) {
+      constexpr int D = decltype(dbgc)::value;
+      if (bn == 192) {
+        hipLaunchKernelGGL((gemm1x1_ws<192, false, 256, D>), dim3(G), dim3(GS_NT), lds, s, p);
+      } else {
+        // 256-wide: 192-pixel tiles (their own tile count and grid)
+        const int T2 = ((M + 191) / 192) * (p.Cout / bn);
+        int G2 = num_cu < T2 ? num_cu : T2;
+        G2 = G2 >= 8 ? G2 / 8 * 8 : G2;
+        if (p.flags & EPI_RES)
+          hipLaunchKernelGGL((gemm1x1_ws<256, true, 192, D>), dim3(G2), dim3(GS_NT), lds, s, p);
+        else
+          hipLaunchKernelGGL((gemm1x1_ws<256, false, 192, D>), dim3(G2), dim3(GS_NT), lds, s, p);
+      }
+    };
+    if (variant == 21) go(std::integral_constant<int, 1>{});
+    else if (variant == 22) go(std::integral_constant<int, 2>{});
+    else if (variant == 25) go(std::integral_constant<int, 5>{});
+    else if (variant == 24) go(std::integral_constant<int, 4>{});
+    else go(std::integral_constant<int, 0>{});
     return hipGetLastError();
   }
   switch (variant) {   // 0 = the product kernel; 11..17 = diagnostics (DBG = variant - 10)
