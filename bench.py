@@ -33,7 +33,7 @@ PEAK_HBM_GBS = 8000.0       # HBM3E spec
 def _kernel_name(tag, dt):
     kind = tag & 15
     if tag & (1 << 30):
-        return "gemm1x1_wide"
+        return "gemm1x1_ws" if tag & (1 << 17) else "gemm1x1_wide"
     if tag & (1 << 29):
         if tag & (1 << 18):
             return "conv3x3_rw"

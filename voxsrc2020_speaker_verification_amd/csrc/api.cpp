@@ -1643,8 +1643,8 @@ extern "C" int vox_profile(vox_model* m, const float* d_x, int n, int t, int f, 
         tag |= (1 << 28);
       else if (o.type == 20)
         tag |= (1 << 29);
-      else if (o.type == 21)
-        tag |= (1 << 30);
+      else if (o.type == 21)   // bit 17: launched as gemm1x1_ws (the default, gemm_wide.hip)
+        tag |= (1 << 30) | ((m->gemm_var == 0 || m->gemm_var == 1) ? (1 << 17) : 0);
       else if (o.type == 22)
         tag |= (1 << 26) | (1 << 19);
       else if (o.type == 23)
