@@ -1,0 +1,41 @@
+"""Per-step phase timing of bneck_fused block 0 from its shader-clock stamps
+(VOXEMB_BNECK_DBG=256; diagnostics).  Runs one B=256 80x200 forward of
+res2net50_w24_s4_c32 and prints, per wave, the mean cycles of: phase 0 work,
+wait at barrier 1, phase 1 work, wait at barrier 2 (the last bneck launch)."""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+os.environ["VOXEMB_BNECK_DBG"] = "256"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from voxsrc2020_speaker_verification_amd import synth  # noqa: E402
+from voxsrc2020_speaker_verification_amd import _native  # noqa: E402
+from voxsrc2020_speaker_verification_amd.extractor import Extractor  # noqa: E402
+
+blob = bench.weights_blob("res2net50_w24_s4_c32", 80, "/tmp/voxemb_cache")
+ex = Extractor(blob, device=0, precision="bf16")
+x = torch.from_numpy(synth.make_features(256, 200, 80, seed=1)).cuda()
+out = torch.empty((256, ex.dim), dtype=torch.float32, device="cuda")
+ex.run_device(x, out, torch.cuda.current_stream())
+torch.cuda.synchronize()
+lib = _native.lib()
+buf = np.zeros(8 * 512 * 4, dtype=np.uint64)
+rc = lib.vox_debug_bneck_trace(C.c_void_p(buf.ctypes.data), C.c_size_t(buf.nbytes))
+assert rc == 0, rc
+tr = buf.reshape(8, 512, 4).astype(np.int64)
+steps = int((tr[0, :, 0] > 0).sum())
+t = tr[:, :steps]
+print(f"steps {steps}; total {(t[0, -1, 3] - t[0, 0, 0])} clk")
+for w in range(8):
+    p0 = (t[w, :, 1] - t[w, :, 0]).mean()
+    b1 = (t[w, :, 2] - t[w, :, 1]).mean()
+    p1 = (t[w, :, 3] - t[w, :, 2]).mean()
+    b2 = (t[w, 1:, 0] - t[w, :-1, 3]).mean()
+    print(f"wave {w}: phase0 {p0:7.0f}  wait1 {b1:7.0f}  phase1 {p1:7.0f}  wait2 {b2:7.0f}")

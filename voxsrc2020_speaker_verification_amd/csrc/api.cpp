@@ -1664,6 +1664,13 @@ extern "C" int vox_profile(vox_model* m, const float* d_x, int n, int t, int f, 
   return nops;
 }
 
+// diagnostics: bneck_fused clock stamps (8 waves x 512 steps x 4 u64), see bneck.hip
+extern "C" int vox_debug_bneck_trace(void* dst, size_t bytes) {
+  if (!dst) return fail(VOX_EINVAL, "null argument");
+  HIPCHK(bneck_trace_read(dst, bytes));
+  return VOX_OK;
+}
+
 extern "C" int vox_plan_describe(vox_model* m, const float* d_x, int n, int t, int f, char* buf,
                                  size_t cap) {
   if (!m || !d_x) return fail(VOX_EINVAL, "null argument");

@@ -88,6 +88,10 @@ __device__ __forceinline__ bf16x4 add4(bf16x4 a, bf16x4 b) {
   return r;
 }
 
+// diagnostics (VOXEMB_BNECK_DBG bit 256): per-step shader-clock stamps of
+// block 0, [wave][step][start, phase-0 done, phase 1 start, phase-1 done]
+__device__ unsigned long long g_vox_trace[8 * 512 * 4];
+
 template <int CI, int C, int WID, int S, int PT>
 __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
   using K = BneckCfg<CI, C, WID, S, PT>;
@@ -238,10 +242,15 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
 
   // step t (register set P = t & 1): rows a + 1 (input) and c (residual) were
   // requested two steps earlier
+  const bool trace = (q.dbg & 256) && blockIdx.x == 0 && lane == 0;
+  auto stamp = [&](int t, int i) __attribute__((always_inline)) {
+    if (trace && t < 512) g_vox_trace[(wave * 512 + t) * 4 + i] = __builtin_amdgcn_s_memtime();
+  };
   auto step = [&](auto P, int t) __attribute__((always_inline)) {
     const int a = a0 + t;
     const int c = a - K::LAG_C;
     auto& res = resb[P];
+    stamp(t, 0);
     // ---------------- phase 0: 1x1a (row a) | 1x1c (row c)
     if (is_a && !(q.dbg & 1)) {
       const bool inimg = a >= 0 && a < H;
@@ -368,7 +377,9 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
       }
     }
     if (!(q.dbg & 8)) load_res(P, c + 2);
+    stamp(t, 1);
     __syncthreads();
+    stamp(t, 2);
     // ---------------- phase 1: all 3x3 stages, stage k on row a-2k+1
     if (!(q.dbg & 8)) {
       store_in(P);
@@ -444,6 +455,7 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
 #pragma unroll
       for (int j = 0; j < PT; ++j) epilogue(acc[j], 16 * j + col);
     }
+    stamp(t, 3);
     __syncthreads();
   };
   for (int t = 0; t < steps; t += 2) {
@@ -1603,4 +1615,12 @@ hipError_t launch_split_s2(const ChainParams& q, hipStream_t st) {
   return hipErrorInvalidValue;
 }
 
+}  // namespace vox
+
+namespace vox {
+// copy the bneck_fused trace (diagnostics) to host memory
+hipError_t bneck_trace_read(void* dst, size_t bytes) {
+  if (bytes > sizeof(g_vox_trace)) bytes = sizeof(g_vox_trace);
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_vox_trace), bytes, 0, hipMemcpyDeviceToHost);
+}
 }  // namespace vox
