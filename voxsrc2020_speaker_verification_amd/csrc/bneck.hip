@@ -88,6 +88,9 @@ __device__ __forceinline__ bf16x4 add4(bf16x4 a, bf16x4 b) {
   return r;
 }
 
+__device__ uint4 g_vox_zero[4] = {};   // source of the row loads outside the image
+__device__ uint4 g_vox_sink[64];       // destination of masked lanes' stores
+
 // diagnostics (VOXEMB_BNECK_DBG bit 256): per-step shader-clock stamps of
 // block 0, [wave][step][start, phase-0 done, phase 1 start, phase-1 done]
 __device__ unsigned long long g_vox_trace[8 * 512 * 4];
@@ -196,15 +199,25 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
   // ---- input rows: global -> registers (prefetch) -> LDS
   // two register sets each for the input rows and the residual rows: a row is
   // requested two steps before it is used (HBM latency under load exceeds a step)
-  uint4 inr[2][K::IREG];
+  vu32x4 inr[2][K::IREG];
+  const int nres = is_c ? PT : 0;                               // residual loads per step
+  const int nst = ((q.dbg & 256) && blockIdx.x == 0) ? 1 : 0;  // trace stamps (stores)
+  // Every global access of the row loop is issued as inline asm with the
+  // wave's vmcnt counted by hand (device_common.h vld16 / vst16 / vm_wait):
+  // compiler-placed waits fell back to vmcnt(0) before the staging writes,
+  // holding every wave on its in-flight 1x1c stores and residual prefetches.
+  // Each load is always issued (rows outside the image read a zero line), so
+  // the per-step op counts are wave-uniform:
+  //   phase 0: 1x1c waves: ns stores (PT when row c is owned, else 0) then PT
+  //            residual loads (row c+2); phase 1: IREG input loads (row a+3).
+  const bf16_t* zline = reinterpret_cast<const bf16_t*>(g_vox_zero);
   auto load_in = [&](auto P, int r) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < K::IREG; ++i) {
-      const int c = tid + i * NT;
+      int c = tid + i * NT;
       const int px = c / K::CU, u = c - px * K::CU;
-      inr[P][i] = make_uint4(0, 0, 0, 0);
-      if (c < 16 * PT * K::CU && px < W && r >= 0 && r < H)
-        inr[P][i] = *reinterpret_cast<const uint4*>(X + (img + (size_t)r * W + px) * CI + u * 8);
+      const bool ok = c < 16 * PT * K::CU && px < W && r >= 0 && r < H;
+      inr[P][i] = vld16(ok ? (const void*)(X + (img + (size_t)r * W + px) * CI + u * 8) : zline);
     }
   };
   auto store_in = [&](auto P) __attribute__((always_inline)) {
@@ -212,19 +225,21 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
     for (int i = 0; i < K::IREG; ++i) {
       const int c = tid + i * NT;
       const int px = c / K::CU, u = c - px * K::CU;
-      if (c < 16 * PT * K::CU) *reinterpret_cast<uint4*>(inb + px * K::ISTR + u * 16) = inr[P][i];
+      vm_launder(inr[P][i]);
+      if (c < 16 * PT * K::CU) *reinterpret_cast<vu32x4*>(inb + px * K::ISTR + u * 16) = inr[P][i];
     }
   };
-  bf16x8 resb[2][PT];
+  vu32x4 resb[2][PT];
   auto load_res = [&](auto P, int r) __attribute__((always_inline)) {
+    if (!is_c) return;
 #pragma unroll
     for (int j = 0; j < PT; ++j) {
       const int px = 16 * j + col;
       // identity: this lane's 8 residual channels; projection: its B chunk of
       // the (CI = 32)-channel input row, for the shortcut MFMAs
       const int cho = K::PROJ ? 8 * g : 32 * pq + 8 * g;
-      resb[P][j] = (is_c && r >= h0 && r < h1 && px < W)
-                   ? ld16(X + (img + (size_t)r * W + px) * CI + cho) : bf16x8{};
+      const bool ok = r >= h0 && r < h1 && px < W;
+      resb[P][j] = vld16(ok ? (const void*)(X + (img + (size_t)r * W + px) * CI + cho) : zline);
     }
   };
 
@@ -233,12 +248,14 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
   using P0 = std::integral_constant<int, 0>;
   using P1 = std::integral_constant<int, 1>;
   load_in(P0{}, a0);
+  vm_wait(0);
   store_in(P0{});
   load_in(P0{}, a0 + 1);
   load_in(P1{}, a0 + 2);
   load_res(P0{}, a0 - K::LAG_C);
   load_res(P1{}, a0 - K::LAG_C + 1);
   __syncthreads();
+  int ns_prev = 0;   // stores this wave issued in the previous step
 
   // step t (register set P = t & 1): rows a + 1 (input) and c (residual) were
   // requested two steps earlier
@@ -250,6 +267,8 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
     const int a = a0 + t;
     const int c = a - K::LAG_C;
     auto& res = resb[P];
+    const bool cstep = is_c && c >= h0 && c < h1 && !(q.dbg & 2);
+    const int ns_cur = cstep ? PT : 0;
     stamp(t, 0);
     // ---------------- phase 0: 1x1a (row a) | 1x1c (row c)
     if (is_a && !(q.dbg & 1)) {
@@ -300,7 +319,12 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
         epi(a0, a1, px);
         if (two) epi(c0, c1, px + 16);
       }
-    } else if (is_c && c >= h0 && c < h1 && !(q.dbg & 2)) {
+    } else if (cstep) {
+      // residual row c (loaded at step t-2): younger are that step's trace
+      // stamps and input loads, step t-1's stores, residual and input loads
+      vm_wait(t < 2 ? 0 : 2 * K::IREG + PT + ns_prev + 7 * nst);
+#pragma unroll
+      for (int j = 0; j < PT; ++j) vm_launder(res[j]);
       // B chunk s of lane group g: concat channel 32s+8g -> (plane, offset)
       const char* src[K::KSC];
 #pragma unroll
@@ -345,12 +369,8 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
           o[4 + e] = (bf16_t)v1;
         }
         o = relu_bf16(o);
-        if (q.dbg & 16) {   // diagnostics: no output stores / all to one line
-        } else if (q.dbg & 32) {
-          if (px < W) *reinterpret_cast<bf16x8*>(Y + lane * 8) = o;
-        } else if (px < W) {
-          *reinterpret_cast<bf16x8*>(Y + (img + (size_t)c * W + px) * C + ch) = o;
-        }
+        vst16(px < W ? (void*)(Y + (img + (size_t)c * W + px) * C + ch) : (void*)&g_vox_sink[lane],
+              __builtin_bit_cast(vu32x4, o));
       };
 #pragma unroll
       for (int j = 0; j < PT; j += 2) {
@@ -372,8 +392,8 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
             c1 = mfma_step(w1[s][1], bq[s], c1);
           }
         }
-        epi(a0, a1, res[j], px);
-        if (two) epi(c0, c1, res[(j + 1) < PT ? j + 1 : j], px + 16);
+        epi(a0, a1, __builtin_bit_cast(bf16x8, res[j]), px);
+        if (two) epi(c0, c1, __builtin_bit_cast(bf16x8, res[(j + 1) < PT ? j + 1 : j]), px + 16);
       }
     }
     if (!(q.dbg & 8)) load_res(P, c + 2);
@@ -382,9 +402,13 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
     stamp(t, 2);
     // ---------------- phase 1: all 3x3 stages, stage k on row a-2k+1
     if (!(q.dbg & 8)) {
+      // input row a+1 (loaded at step t-2): younger are step t-1's and this
+      // step's stores and residual loads, step t-1's input loads, 8 stamps
+      vm_wait(t < 2 ? 0 : K::IREG + ns_prev + ns_cur + 2 * nres + 8 * nst);
       store_in(P);
       load_in(P, a + 3);
     }
+    ns_prev = ns_cur;
     if (chain_wave && !(q.dbg & 4)) {
       const int k = ck;
       const int co = 16 * ci + 4 * g;

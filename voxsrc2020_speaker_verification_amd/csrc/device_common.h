@@ -44,6 +44,44 @@ __device__ __forceinline__ bf16x8 relu_bf16(bf16x8 v) {
   return __builtin_bit_cast(bf16x8, s);
 }
 
+// Global loads / stores issued as inline asm, for kernels that count their
+// own vmcnt: the compiler's waitcnt pass cannot prove which older loads a later
+// use depends on across role branches and falls back to vmcnt(0), which also
+// waits for every store the wave has in flight.  A value loaded with vld16 is
+// valid only after vm_wait(n) (n = this wave's vector-memory ops issued after
+// it) and vm_launder(v) (so the compiler does not hoist uses above the wait).
+typedef unsigned vu32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ vu32x4 vld16(const void* p) {
+  vu32x4 v;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+// the trailing s_nop keeps the next instruction from overwriting the data
+// registers before the store has read them
+__device__ __forceinline__ void vst16(void* p, vu32x4 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" : : "v"(p), "v"(v) : "memory");
+}
+template <typename T>
+__device__ __forceinline__ void vm_launder(T& v) {
+  asm volatile("" : "+v"(v));
+}
+#define VOX_VMW(n) \
+  case n: asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory"); break;
+// s_waitcnt vmcnt(n) for a wave-uniform n (a scalar branch to the immediate form)
+__device__ __forceinline__ void vm_wait(int n) {
+  switch (n) {
+    VOX_VMW(0) VOX_VMW(1) VOX_VMW(2) VOX_VMW(3) VOX_VMW(4) VOX_VMW(5) VOX_VMW(6) VOX_VMW(7)
+    VOX_VMW(8) VOX_VMW(9) VOX_VMW(10) VOX_VMW(11) VOX_VMW(12) VOX_VMW(13) VOX_VMW(14)
+    VOX_VMW(15) VOX_VMW(16) VOX_VMW(17) VOX_VMW(18) VOX_VMW(19) VOX_VMW(20) VOX_VMW(21)
+    VOX_VMW(22) VOX_VMW(23) VOX_VMW(24) VOX_VMW(25) VOX_VMW(26) VOX_VMW(27) VOX_VMW(28)
+    VOX_VMW(29) VOX_VMW(30) VOX_VMW(31) VOX_VMW(32) VOX_VMW(33) VOX_VMW(34) VOX_VMW(35)
+    VOX_VMW(36) VOX_VMW(37) VOX_VMW(38) VOX_VMW(39) VOX_VMW(40)
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+  __builtin_amdgcn_sched_barrier(0);
+}
+#undef VOX_VMW
+
 __device__ __forceinline__ f32x4 mfma_step(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
