@@ -89,7 +89,6 @@ __device__ __forceinline__ bf16x4 add4(bf16x4 a, bf16x4 b) {
 }
 
 __device__ uint4 g_vox_zero[4] = {};   // source of the row loads outside the image
-__device__ uint4 g_vox_sink[64];       // destination of masked lanes' stores
 
 // diagnostics (VOXEMB_BNECK_DBG bit 256): per-step shader-clock stamps of
 // block 0, [wave][step][start, phase-0 done, phase 1 start, phase-1 done]
@@ -247,6 +246,15 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
   const int steps = (h1 - h0) + 3 * (S - 1);
   using P0 = std::integral_constant<int, 0>;
   using P1 = std::integral_constant<int, 1>;
+  // the weights land here: otherwise the compiler, which does not see the asm
+  // loads, re-places its waits for them inside the row loop every step, where
+  // they drain the row prefetches too
+#pragma unroll
+  for (int s = 0; s < K::KSW; ++s) { vm_launder(w1[s][0]); vm_launder(w1[s][1]); }
+  vm_launder(wp[0]);
+  vm_launder(wp[1]);
+#pragma unroll
+  for (int s = 0; s < KST; ++s) vm_launder(wb[s]);
   load_in(P0{}, a0);
   vm_wait(0);
   store_in(P0{});
@@ -369,8 +377,8 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
           o[4 + e] = (bf16_t)v1;
         }
         o = relu_bf16(o);
-        vst16(px < W ? (void*)(Y + (img + (size_t)c * W + px) * C + ch) : (void*)&g_vox_sink[lane],
-              __builtin_bit_cast(vu32x4, o));
+        // lane col 0 (px = 16 j < W) is always active: one store per tile
+        if (px < W) vst16(Y + (img + (size_t)c * W + px) * C + ch, __builtin_bit_cast(vu32x4, o));
       };
 #pragma unroll
       for (int j = 0; j < PT; j += 2) {
@@ -1420,9 +1428,14 @@ __global__ __launch_bounds__((S2FusedCfg<CI, WID, S, WIN>::NT)) void s2_fused(Ch
     ktl[l * K::KP * 2 + st] = (unsigned short)(dyi * ROWB + off + ASTR + 2 * (l & 15) * ASTR);
   }
 
-  // two input rows per step: global -> registers (one step ahead) -> LDS
-  uint4 xr[K::XREG];
+  // two input rows per step: global -> registers (one step ahead) -> LDS.
+  // The row loads are inline asm (device_common.h vld16; rows outside the
+  // image read a zero line) and waited for by hand right after the phase-A
+  // barrier, where only they and the previous step's output stores are in
+  // flight: compiler-placed waits drained them at the top of phase A.
+  vu32x4 xr[K::XREG];
   const int ldx = q.ldx;
+  const bf16_t* zline = reinterpret_cast<const bf16_t*>(g_vox_zero);
   auto load_x = [&](int r0) __attribute__((always_inline)) {
     const bf16_t* base = X + (img + (size_t)r0 * W) * ldx;
 #pragma unroll
@@ -1432,9 +1445,8 @@ __global__ __launch_bounds__((S2FusedCfg<CI, WID, S, WIN>::NT)) void s2_fused(Ch
       const int rr = c / (W * CU), cc = c - rr * (W * CU);
       const int px = cc / CU, u = cc - px * CU;
       const int r = r0 + rr;
-      xr[i] = make_uint4(0, 0, 0, 0);
-      if (rr < 2 && r >= 0 && r < H)
-        xr[i] = *reinterpret_cast<const uint4*>(base + (rr * W + px) * ldx + u * 8);
+      const bool ok = rr < 2 && r >= 0 && r < H;
+      xr[i] = vld16(ok ? (const void*)(base + (rr * W + px) * ldx + u * 8) : zline);
     }
   };
   auto store_x = [&]() __attribute__((always_inline)) {
@@ -1444,12 +1456,19 @@ __global__ __launch_bounds__((S2FusedCfg<CI, WID, S, WIN>::NT)) void s2_fused(Ch
       asm volatile("" : "+v"(c));
       const int rr = c / (W * CU), cc = c - rr * (W * CU);
       const int px = cc / CU, u = cc - px * CU;
+      vm_launder(xr[i]);
       if (rr < 2)
-        *reinterpret_cast<uint4*>(inb + rr * K::INROW + ((u >> 1) * K::SPX + 2 * px + (u & 1)) * 16) = xr[i];
+        *reinterpret_cast<vu32x4*>(inb + rr * K::INROW + ((u >> 1) * K::SPX + 2 * px + (u & 1)) * 16) = xr[i];
     }
   };
 
+  // the weights land here, not at a compiler wait inside the row loop
+#pragma unroll
+  for (int s = 0; s < KST; ++s) vm_launder(wb[s]);
+#pragma unroll
+  for (int s = 0; s < K::KSA; ++s) vm_launder(w1[s]);
   load_x(2 * (g0 - 1));
+  vm_wait(0);
   store_x();
   __syncthreads();
   for (int ho = g0 - 1; ho < g1; ++ho) {
@@ -1500,6 +1519,10 @@ __global__ __launch_bounds__((S2FusedCfg<CI, WID, S, WIN>::NT)) void s2_fused(Ch
       }
     }
     __syncthreads();
+    if (!(q.dbg & 8)) {   // input rows 2ho+2, 2ho+3: phase A is done with the staging
+      vm_wait(0);
+      store_x();
+    }
     // ---------------- phase B: output row ho from A-rows 2ho-1 .. 2ho+1
     if (ho >= g0 && !(q.dbg & 2)) {
       const int rb0 = __builtin_amdgcn_readfirstlane(((2 * ho - 1 + 840) % 3) * ROWB);
@@ -1584,7 +1607,6 @@ __global__ __launch_bounds__((S2FusedCfg<CI, WID, S, WIN>::NT)) void s2_fused(Ch
         }
       }
     }
-    if (!(q.dbg & 8)) store_x();   // input rows 2ho+2, 2ho+3 (phase A of this step is done with the staging)
     __syncthreads();
   }
 }

@@ -50,16 +50,18 @@ __device__ __forceinline__ bf16x8 relu_bf16(bf16x8 v) {
 // waits for every store the wave has in flight.  A value loaded with vld16 is
 // valid only after vm_wait(n) (n = this wave's vector-memory ops issued after
 // it) and vm_launder(v) (so the compiler does not hoist uses above the wait).
+// No "memory" clobbers: the kernels never read back what these touch, and a
+// clobber would pin every LDS access around each store.
 typedef unsigned vu32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ vu32x4 vld16(const void* p) {
   vu32x4 v;
-  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p));
   return v;
 }
 // the trailing s_nop keeps the next instruction from overwriting the data
 // registers before the store has read them
 __device__ __forceinline__ void vst16(void* p, vu32x4 v) {
-  asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" : : "v"(p), "v"(v) : "memory");
+  asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" : : "v"(p), "v"(v));
 }
 template <typename T>
 __device__ __forceinline__ void vm_launder(T& v) {
