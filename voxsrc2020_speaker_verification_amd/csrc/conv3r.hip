@@ -74,7 +74,6 @@ __device__ __forceinline__ void cr_wait_vm(int n) {
 }  // namespace
 
 __device__ uint4 g_cr_zero[4] = {};
-__device__ uint4 g_cr_sink[64];
 
 template <int W>
 struct CrCfg {
@@ -163,8 +162,13 @@ __global__ __launch_bounds__(CR_NT) void conv3x3_rw(ConvParams p) {
     const int p0 = t * CR_TP;
     const bf16_t* src = zero;
     if (q < K::WPC) {
-      int u = 64 * q + lane;
-      asm volatile("" : "+v"(u));   // recomputed per tile: no per-piece state held in registers
+      // recomputed per tile from the laundered lane id: no per-piece state
+      // held in registers (laundering the sum instead made the compiler keep
+      // each piece's sum in scratch and reload it under a vmcnt(0) that
+      // serialised the DMA issue)
+      int u = lane;
+      asm volatile("" : "+v"(u));
+      u += 64 * q;
       const int sp = u / SPW, rem = u - sp * SPW;
       const int slot = rem >> 1, c = 2 * sp + (rem & 1);
       const int wr_ = slot / SW, sc = slot - wr_ * SW;
@@ -173,8 +177,9 @@ __global__ __launch_bounds__(CR_NT) void conv3x3_rw(ConvParams p) {
         src = X + ((size_t)n * HW + row * W + wc) * p.ldx + c * 8;
       if (DBG & 1) src = X + ((size_t)n * HW + p0) * p.ldx + u * 8;
     } else if (HAS_Z) {
-      int u = 64 * (q - K::WPC) + lane;
+      int u = lane;
       asm volatile("" : "+v"(u));
+      u += 64 * (q - K::WPC);
       const int px = u / CR_NCH, c = u - px * CR_NCH;
       const int pix = min(p0 + px, HW - 1);
       src = XZ + ((size_t)n * HW + pix) * p.ldr + c * 8;
@@ -216,18 +221,21 @@ __global__ __launch_bounds__(CR_NT) void conv3x3_rw(ConvParams p) {
     const char* xzl = xzb + (tj & 1) * K::XZB;
 #pragma unroll
     for (int i = 0; i < CR_TP * CR_NCH / CR_NT; ++i) {
-      const int c = tid + CR_NT * i;
+      int c = tid;
+      asm volatile("" : "+v"(c));   // nothing per-pass held in registers (or scratch)
+      c += CR_NT * i;
       const int px = c / CR_NCH, u = c - px * CR_NCH;
       const bool in = p0 + px < HW && !(DBG & 8);
       const size_t pix = (size_t)n * HW + p0 + px;
       const bf16x8 y = *reinterpret_cast<const bf16x8*>(ys + px * K::YST + u * 16);
-      cr_st16(in ? (void*)(Y + pix * p.ldy + u * 8) : (void*)&g_cr_sink[lane], __builtin_bit_cast(u32x4, y));
+      // (masked lanes skip the store: the tile's closing vmcnt(0) needs no count)
+      if (in) cr_st16(Y + pix * p.ldy + u * 8, __builtin_bit_cast(u32x4, y));
       if (HAS_Z) {
         const bf16x8 xv = *reinterpret_cast<const bf16x8*>(xzl + px * (CR_C * 2) + u * 16);
         bf16x8 zv;
 #pragma unroll
         for (int e = 0; e < 8; ++e) zv[e] = (bf16_t)((float)xv[e] + (float)y[e]);
-        cr_st16(in ? (void*)(Z + pix * p.ldy2 + u * 8) : (void*)&g_cr_sink[lane], __builtin_bit_cast(u32x4, zv));
+        if (in) cr_st16(Z + pix * p.ldy2 + u * 8, __builtin_bit_cast(u32x4, zv));
       }
     }
   };
