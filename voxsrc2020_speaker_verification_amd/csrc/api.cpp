@@ -156,6 +156,7 @@ struct ConvW {
   std::shared_ptr<DevBuf> w;         // [groups][coutp][kp] in the model dtype
   std::shared_ptr<DevBuf> wtc;       // bf16 [coutp][taps*cin] for conv_win (groups == 1)
   std::shared_ptr<DevBuf> wpair;     // bf16 [coutp][kp] paired-row layout for conv1x1_rr
+  std::shared_ptr<DevBuf> wblk;      // wpair re-blocked for gemm1x1_ws (contiguous 1-KB DMA pieces)
   std::shared_ptr<DevBuf> wstem;     // fp32 [9][cout] for the 1-channel 3x3 stem kernel
   std::shared_ptr<DevBuf> wgc;       // bf16 [C/16][NM][64][8] expanded grouped 3x3 (gconv.hip)
   std::shared_ptr<DevBuf> mean, inv; // optional epilogue BN (cout*groups)
@@ -229,6 +230,7 @@ struct vox_model {
   bool no_gemm = false;        // VOXEMB_NO_GEMM=1: disable gemm1x1_lds
   bool no_gemm_pipe = false;   // VOXEMB_NO_GEMM_PIPE=1: gemm1x1_lds instead of gemm1x1_pipe
   bool no_gemm_wide = false;   // VOXEMB_NO_GEMM_WIDE=1: gemm1x1_pipe instead of gemm1x1_wide
+  bool no_wblk = false;        // VOXEMB_NO_WBLK=1: gemm1x1_ws reads the paired-row weights
   bool no_s2_fused = false;    // VOXEMB_NO_S2_FUSED=1: 1x1a + split_s2_rows instead of s2_fused
   bool no_chain_fused = false; // VOXEMB_NO_CHAIN_FUSED=1: 1x1a + chain_rows instead of chain_fused
   // VOXEMB_CONV3_WIN=1: window-staged conv3x3_win for the w=96 stride-1 branches
@@ -313,6 +315,25 @@ static int make_conv(vox_model* m, const HostTensor& k, int groups, const HostTe
     out.wpair = std::make_shared<DevBuf>();
     HIPCHK(out.wpair->ensure(h.size() * 2));
     HIPCHK(hipMemcpy(out.wpair->p, h.data(), h.size() * 2, hipMemcpyHostToDevice));
+    if (out.kp % 32 == 0) {
+      // gemm1x1_ws weight pieces: block (16-row group rb, k-step kk) is the 1 KB a
+      // loader lane set writes into LDS, lane l -> row 16rb + l/4, chunk
+      // (l & 3) ^ f(row), f(r) = (4 - ((r >> 2) & 3)) & 3 (gemm_wide.hip gw_swz):
+      // one contiguous read of eight full cache lines instead of 16 half lines
+      const int KT = out.kp / 32;
+      std::vector<uint16_t> b(h.size());
+      for (int rb = 0; rb < rows / 16; ++rb)
+        for (int kk = 0; kk < KT; ++kk)
+          for (int l = 0; l < 64; ++l) {
+            const int row = 16 * rb + l / 4;
+            const int c = (l & 3) ^ ((4 - ((row >> 2) & 3)) & 3);
+            for (int e = 0; e < 8; ++e)
+              b[(((size_t)rb * KT + kk) * 64 + l) * 8 + e] = h[(size_t)row * out.kp + kk * 32 + c * 8 + e];
+          }
+      out.wblk = std::make_shared<DevBuf>();
+      HIPCHK(out.wblk->ensure(b.size() * 2));
+      HIPCHK(hipMemcpy(out.wblk->p, b.data(), b.size() * 2, hipMemcpyHostToDevice));
+    }
   }
   if (dt == BF16 && groups > 1 && kh == 3 && kw == 3 && cin == cout &&
       (cin == 4 || cin == 8 || cin == 16 || cin == 32) && (cout * groups) % 64 == 0) {
@@ -608,7 +629,10 @@ static void emit_conv(Builder& B, const ConvW& cw, Act x, const void* x2, int ld
       if (!B.m->no_gemm_pipe && gemm_pipe_ok(p)) op.type = 18;
       // wide-tile variant (gemm_wide.hip): 256 x 256 / 256 x 192 tiles, residual
       // streamed through the DMA ring
-      if (!B.m->no_gemm_wide && gemm_wide_bn(p)) op.type = 21;
+      if (!B.m->no_gemm_wide && gemm_wide_bn(p)) {
+        op.type = 21;
+        p.wblk = (cw.wblk && !B.m->no_wblk) ? cw.wblk->p : nullptr;
+      }
     }
   }
   // bf16 1x1 with a BN+ReLU input prologue (DPN bn_relu_conv): the pipelined
@@ -1460,6 +1484,7 @@ extern "C" int vox_load_blob(const void* blob, size_t nbytes, int device, int pr
   if (const char* e = std::getenv("VOXEMB_NO_GEMM")) m->no_gemm = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_NO_GEMM_PIPE")) m->no_gemm_pipe = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_NO_GEMM_WIDE")) m->no_gemm_wide = std::atoi(e) != 0;
+  if (const char* e = std::getenv("VOXEMB_NO_WBLK")) m->no_wblk = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_NO_GRAPH")) m->use_graph = std::atoi(e) == 0;
   if (const char* e = std::getenv("VOXEMB_NO_GCONV")) m->no_gconv = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_NO_CONV3")) m->no_conv3 = std::atoi(e) != 0;

@@ -371,6 +371,7 @@ __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
   constexpr int NR = RES ? NJ : 0;           // residual phases (64 pixels x 256 couts each)
   constexpr int NLR = 32 / GS_NL;            // residual pieces per loader wave
   static_assert(GRP % GS_NL == 0, "groups per loader");
+  static_assert(BN % 64 == 0, "weight pieces are the first BN/64 of a loader");
   static_assert(!RES || BN == 256, "residual phases: 256 couts");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
@@ -424,6 +425,11 @@ __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
   if (loader) {
     // ---- loader waves: groups gi = lw + 4 i of every step
     const bf16_t* src[NLL];
+    // weight pieces (i < BN/64: groups gi < BN/16) from the re-blocked copy when
+    // present: one contiguous 1-KB block per (16 rows, k-step), already in LDS order
+    const bf16_t* __restrict__ Wb = reinterpret_cast<const bf16_t*>(p.wblk);
+    const bool blk = Wb != nullptr && !(DBG & 4);
+    const int wstep = blk ? 512 : 32;   // elements per k-step of a weight piece
     int l_tile = 0, l_k = 0, l_co0 = 0, l_px0 = 0;
     auto set_load_tile = [&](int tj) {
       const int lid = t_first + tj * t_step;
@@ -435,7 +441,9 @@ __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
         // DBG 4 (timing only): 8 rows x 128 B per piece instead of 16 x 64 B
         const int row = (DBG & 4) ? 16 * gi + 2 * (lane >> 3) : 16 * gi + (lane >> 2);
         const int c = (DBG & 4) ? (lane & 7) : ((lane & 3) ^ gw_swz(row));
-        if (row < BN) {
+        if (row < BN && blk) {
+          src[i] = Wb + ((size_t)((l_co0 >> 4) + gi) * KT) * 512 + lane * 8;
+        } else if (row < BN) {
           src[i] = Wt + (size_t)(l_co0 + row) * p.kp + c * 8;
         } else {
           const int pix = min(l_px0 + row - BN, M - 1);
@@ -452,7 +460,8 @@ __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
 #pragma unroll
         for (int i = 0; i < NLL; ++i) {
           const int gi = lw + GS_NL * i;
-          if (!(DBG & 2)) gw_glds16(src[i] + l_k * 32, lds0 + (uint32_t)slot * GW_SLOT + (uint32_t)gi * 1024u);
+          const int kst = i < BN / 64 ? wstep : 32;   // gi < BN/16 <=> i < BN/64
+          if (!(DBG & 2)) gw_glds16(src[i] + l_k * kst, lds0 + (uint32_t)slot * GW_SLOT + (uint32_t)gi * 1024u);
         }
         n = (DBG & 2) ? 0 : NLL;
       } else if (RES) {

@@ -36,6 +36,9 @@ struct ConvParams {
   int cblocks;                             // cout blocks per group (gridDim.y = groups*cblocks)
   // window-staged kernel (conv_win) geometry, see launch_conv_win
   int win_lo, win_len, win_kc, win_astr, win_wstr, win_lds;
+  // gemm1x1_ws: paired-row bf16 weights re-blocked as [rows/16][kp/32][1 KB], each
+  // 1-KB block one DMA piece in LDS order (swizzle applied), or null
+  const void* wblk;
 };
 
 struct ConvLaunch {
