@@ -1139,8 +1139,13 @@ __global__ __launch_bounds__(256) void stem_conv1(const float* __restrict__ x, i
   __syncthreads();
   const int64_t pix = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (pix >= (int64_t)N * H * W) return;
-  const int wi = (int)(pix % W);
-  const int hi = (int)((pix / W) % H);
+  // (h, w) with 32-bit divisions whenever the pixel count allows (the 64-bit
+  // ones cost more than the stem's loads)
+  const int64_t npix = (int64_t)N * H * W;
+  const unsigned hw = npix < ((int64_t)1 << 32) ? (unsigned)pix % (unsigned)(H * W)
+                                                : (unsigned)(pix % ((int64_t)H * W));
+  const int hi = (int)(hw / (unsigned)W);
+  const int wi = (int)(hw - (unsigned)hi * (unsigned)W);
   float v[9];
 #pragma unroll
   for (int t = 0; t < 9; ++t) {
@@ -1405,13 +1410,16 @@ __global__ __launch_bounds__(256) void avgpool3s2_k(const T* __restrict__ x, int
 __global__ __launch_bounds__(256) void avgpool3s2_v8(const bf16_t* __restrict__ x, int ldx, int N,
                                                      int H, int W, int C8, bf16_t* __restrict__ y,
                                                      int ldy, int Ho, int Wo) {
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (int64_t)N * Ho * Wo * C8) return;
-  const int c = (int)(idx % C8) * 8;
-  const int64_t pix = idx / C8;
-  const int wo = (int)(pix % Wo);
-  const int ho = (int)((pix / Wo) % Ho);
-  const int n = (int)(pix / ((int64_t)Wo * Ho));
+  // 32-bit index math (the launcher guarantees N*Ho*Wo*C8 < 2^31): the 64-bit
+  // divisions cost more than the loads
+  const unsigned idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (unsigned)(N * Ho * Wo * C8)) return;
+  const unsigned pix = idx / (unsigned)C8;
+  const int c = (int)(idx - pix * (unsigned)C8) * 8;
+  const unsigned nh = pix / (unsigned)Wo;
+  const int wo = (int)(pix - nh * (unsigned)Wo);
+  const int n = (int)(nh / (unsigned)Ho);
+  const int ho = (int)(nh - (unsigned)n * (unsigned)Ho);
   float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   for (int ky = 0; ky < 3; ++ky) {
     const int hi = 2 * ho - 1 + ky;
@@ -1427,12 +1435,13 @@ __global__ __launch_bounds__(256) void avgpool3s2_v8(const bf16_t* __restrict__ 
   bf16x8 o;
 #pragma unroll
   for (int e = 0; e < 8; ++e) o[e] = (bf16_t)(s[e] / 9.0f);
-  *reinterpret_cast<uint4*>(y + pix * ldy + c) = __builtin_bit_cast(uint4, o);
+  *reinterpret_cast<uint4*>(y + (size_t)pix * ldy + c) = __builtin_bit_cast(uint4, o);
 }
 
 hipError_t launch_avgpool3s2(DType t, const void* x, int ldx, int N, int H, int W, int C,
                              void* y, int ldy, int Ho, int Wo, hipStream_t s) {
-  if (t == BF16 && C % 8 == 0 && ldx % 8 == 0 && ldy % 8 == 0) {
+  if (t == BF16 && C % 8 == 0 && ldx % 8 == 0 && ldy % 8 == 0 &&
+      (int64_t)N * Ho * Wo * (C / 8) < (int64_t)1 << 31) {
     const int64_t n = (int64_t)N * Ho * Wo * (C / 8);
     hipLaunchKernelGGL(avgpool3s2_v8, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
                        (const bf16_t*)x, ldx, N, H, W, C / 8, (bf16_t*)y, ldy, Ho, Wo);
