@@ -1290,11 +1290,32 @@ __global__ __launch_bounds__(64 * TS) void stats_pool_k(const T* __restrict__ x,
   }
   const size_t rowstride = (size_t)W * C;
   const T* base = x + ((size_t)n * H * W + w) * C + (size_t)ch * VN;
+  // the first RM rows of this slice stay in registers for the second pass (the
+  // re-read was the kernel's second HBM/L2 stream); same summation order
+  constexpr int RM = 8;
+  float v[RM][VN];
   float s[VN];
 #pragma unroll
   for (int e = 0; e < VN; ++e) s[e] = 0.f;
   if (valid) {
-    for (int h = ts; h < H; h += TS) {
+#pragma unroll
+    for (int i = 0; i < RM; ++i) {
+      const int h = ts + i * TS;
+      if (h < H) {
+        const T* q = base + (size_t)h * rowstride;
+        if constexpr (sizeof(T) == 2 && VN == 8) {
+          const bf16x8 r = ld16(q);
+#pragma unroll
+          for (int e = 0; e < VN; ++e) v[i][e] = (float)r[e];
+        } else {
+#pragma unroll
+          for (int e = 0; e < VN; ++e) v[i][e] = (float)q[e];
+        }
+#pragma unroll
+        for (int e = 0; e < VN; ++e) s[e] += v[i][e];
+      }
+    }
+    for (int h = ts + RM * TS; h < H; h += TS) {
       const T* q = base + (size_t)h * rowstride;
 #pragma unroll
       for (int e = 0; e < VN; ++e) s[e] += (float)q[e];
@@ -1316,7 +1337,17 @@ __global__ __launch_bounds__(64 * TS) void stats_pool_k(const T* __restrict__ x,
 #pragma unroll
   for (int e = 0; e < VN; ++e) { mu[e] = mu_s[cx][e]; s[e] = 0.f; }
   if (valid) {
-    for (int h = ts; h < H; h += TS) {
+#pragma unroll
+    for (int i = 0; i < RM; ++i) {
+      if (ts + i * TS < H) {
+#pragma unroll
+        for (int e = 0; e < VN; ++e) {
+          float d = v[i][e] - mu[e];
+          s[e] += d * d;
+        }
+      }
+    }
+    for (int h = ts + RM * TS; h < H; h += TS) {
       const T* q = base + (size_t)h * rowstride;
 #pragma unroll
       for (int e = 0; e < VN; ++e) {
