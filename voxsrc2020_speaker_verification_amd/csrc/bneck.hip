@@ -885,10 +885,13 @@ __global__ __launch_bounds__((ChainFusedCfg<CI, WID, S, PT>::NT)) void chain_fus
   const int steps = (h1 - h0) + 3 * (S - 1) - 1;   // as chain_rows
   load_x(a0);
   store_x();
+  load_x(a0 + 1);
   __syncthreads();
   for (int t = 0; t < steps; ++t) {
     const int a = a0 + t;
-    load_x(a + 1);   // lands during phase A, goes to the staging after it
+    // input row a+1 was requested right after the previous step's staging
+    // store, so it has phase B of step t-1 and phase A of this step to land
+    // (requested at the top of the step it had phase A only)
     // ---------------- phase A: 1x1a of A-row a -> rings / x_S
     {
       const int ch = 32 * (t16 >> 1) + 8 * g + 4 * (t16 & 1);
@@ -951,7 +954,8 @@ __global__ __launch_bounds__((ChainFusedCfg<CI, WID, S, PT>::NT)) void chain_fus
       }
     }
     __syncthreads();
-    store_x();   // input row a+1: phase A is done with the staging; xr dies here
+    store_x();   // input row a+1: phase A is done with the staging
+    load_x(a + 2);
     // ---------------- phase B: chain_rows' stages, stage k on row a-2k+1
     if (role) {
       const int k = ck;
