@@ -926,17 +926,19 @@ __global__ __launch_bounds__((ChainFusedCfg<CI, WID, S, PT>::NT)) void chain_fus
         acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
         bc[j] = frag(0, j);
       }
+      if (!(q.dbg & 128)) {   // (diagnostics: 128 = no phase-A MFMAs)
 #pragma unroll
-      for (int s = 0; s < K::KSA; ++s) {
-        if (s + 1 < K::KSA) {
+        for (int s = 0; s < K::KSA; ++s) {
+          if (s + 1 < K::KSA) {
 #pragma unroll
-          for (int j = 0; j < PT; ++j) bn[j] = frag(s + 1, j);
+            for (int j = 0; j < PT; ++j) bn[j] = frag(s + 1, j);
+          }
+#pragma unroll
+          for (int j = 0; j < PT; ++j) acc[j] = mfma_step(w1[s], bc[j], acc[j]);
+#pragma unroll
+          for (int j = 0; j < PT; ++j) bc[j] = bn[j];
+          __builtin_amdgcn_sched_barrier(0);   // reads stay one k-step ahead
         }
-#pragma unroll
-        for (int j = 0; j < PT; ++j) acc[j] = mfma_step(w1[s], bc[j], acc[j]);
-#pragma unroll
-        for (int j = 0; j < PT; ++j) bc[j] = bn[j];
-        __builtin_amdgcn_sched_barrier(0);   // reads stay one k-step ahead
       }
 #pragma unroll
       for (int j = 0; j < PT; ++j) {
@@ -957,7 +959,9 @@ __global__ __launch_bounds__((ChainFusedCfg<CI, WID, S, PT>::NT)) void chain_fus
     store_x();   // input row a+1: phase A is done with the staging
     load_x(a + 2);
     // ---------------- phase B: chain_rows' stages, stage k on row a-2k+1
-    if (role) {
+    // (VOXEMB_BNECK_DBG diagnostics, garbage out: 16 = wave 8 skips its role,
+    // 32 = wave 1 skips its role, 64 = no phase B)
+    if (role && !((q.dbg & 16) && wave == 8) && !((q.dbg & 32) && wave == 1) && !(q.dbg & 64)) {
       const int k = ck;
       const int co = 16 * ci + 4 * g;
       const int r = a - 2 * k + 1;
