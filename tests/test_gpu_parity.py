@@ -416,6 +416,31 @@ def test_chain_fused_bitwise(weights, name, F, T, N, monkeypatch):
 
 @pytest.mark.parametrize("name,F,T,N", [("res2net50_w24_s4_c32", 80, 200, 16),
                                         ("res2net50_w24_s4_c32", 80, 123, 7),
+                                        ("res2net50_w24_s4_c32", 80, 400, 3),
+                                        ("res2net50_w24_s4_c32", 80, 600, 2),
+                                        ("res2net50_w24_s4_c32", 80, 27, 1),
+                                        ("res2net101_w24_s4_c32_att", 80, 64, 3)])
+def test_conv3_utt_bitwise_pipe(weights, name, F, T, N, monkeypatch):
+    """The utterance-band window 3x3 for the w = 192 branches (window of up to
+    25 rows + halo staged once, weights streamed per k-step, the next branch's
+    addend in place; several bands per utterance at T = 400/600, a 4-row image
+    at T = 27) gives the same bits as conv3x3_pipe."""
+    import torch
+    from voxsrc2020_speaker_verification_amd import synth
+    spec, t, blob = weights(name, F)
+    x = synth.make_features(N, T, F, seed=47)
+    with _extractor(blob, "bf16") as ex:
+        got = ex.run(x)
+        assert sum(l.startswith("conv3utt") for l in ex.describe(torch.from_numpy(x).cuda())) >= 6
+    monkeypatch.setenv("VOXEMB_NO_CONV3_UTT", "1")
+    with _extractor(blob, "bf16") as ex:
+        ref = ex.run(x)
+        assert not any(l.startswith("conv3utt") for l in ex.describe(torch.from_numpy(x).cuda()))
+    assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("name,F,T,N", [("res2net50_w24_s4_c32", 80, 200, 16),
+                                        ("res2net50_w24_s4_c32", 80, 123, 7),
                                         ("res2net50_w24_s4_c32", 40, 75, 3),
                                         ("res2net50_w24_s4_c32", 40, 37, 2),
                                         ("res2net50_w24_s4_c32", 80, 27, 1),

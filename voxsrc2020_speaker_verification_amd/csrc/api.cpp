@@ -238,6 +238,7 @@ struct vox_model {
   // B=256 -- twice the K-steps, each paying the ring's fixed per-step cost)
   bool no_conv3_win = true;
   bool no_conv3_rw = false;    // VOXEMB_NO_CONV3_RW=1: conv3x3_pipe for the w = 96 stride-1 branches
+  bool no_conv3_utt = false;   // VOXEMB_NO_CONV3_UTT=1: conv3x3_pipe for the w = 192 stride-1 branches
   bool no_gconv = false;       // VOXEMB_NO_GCONV=1: grouped 3x3 on the generic implicit GEMM
   bool no_conv3 = false;
   bool no_gemm_pro = false;    // VOXEMB_NO_GEMM_PRO=1: prologue 1x1 convs off the pipelined GEMM       // VOXEMB_NO_CONV3=1: Res2Net w>=96 3x3 branches on conv_win/igemm
@@ -1211,6 +1212,8 @@ static int build_res2net(Builder& B, const float* x, int n, int t, float* out) {
           if (ok && !m->no_conv3_win && conv3_win_ok(p)) op.type = 23;
           // ... or with the weights in registers (conv3r.hip)
           else if (ok && !m->no_conv3_rw && conv3_rw_ok(p)) op.type = 25;
+          // w = 192: one utterance band's window staged once, weights streamed (conv3u.hip)
+          else if (ok && !m->no_conv3_utt && conv3_utt_ok(p)) op.type = 26;
           op.flops = 2.0 * n * Ho * Wo * 9.0 * br.cin * br.cout;
           op.bytes = (double)es * ((double)n * H * W * br.cin +
                                    (double)n * Ho * Wo * br.cout * (z ? 3.0 : 1.0));
@@ -1413,6 +1416,7 @@ static hipError_t run_op(vox_model* m, const Op& op, hipStream_t s) {
     case 24: return launch_chain_fused(op.ch, s);
     case 23: return launch_conv3_win(op.cp, m->num_cu, s);
     case 25: return launch_conv3_rw(op.cp, m->num_cu, s);
+    case 26: return launch_conv3_utt(op.cp, m->num_cu, s);
     case 15: return launch_convert_bf16(op.src, (float*)op.dst, op.count, s);
     case 16: return launch_att_bias_tanh((float*)op.dst, (const float*)op.src, op.N, op.H, op.W, op.C, s);
     case 17:
@@ -1501,6 +1505,7 @@ extern "C" int vox_load_blob(const void* blob, size_t nbytes, int device, int pr
   if (const char* e = std::getenv("VOXEMB_NO_CHAIN_FUSED")) m->no_chain_fused = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_CONV3_WIN")) m->no_conv3_win = std::atoi(e) == 0;
   if (const char* e = std::getenv("VOXEMB_NO_CONV3_RW")) m->no_conv3_rw = std::atoi(e) != 0;
+  if (const char* e = std::getenv("VOXEMB_NO_CONV3_UTT")) m->no_conv3_utt = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_BNECK_NSEG")) m->bneck_nseg = std::atoi(e);
   if (const char* e = std::getenv("VOXEMB_BNECK_DBG")) m->bneck_dbg = std::atoi(e);
   if (const char* e = std::getenv("VOXEMB_CHAIN_R")) m->chain_r = std::atoi(e);
@@ -1679,6 +1684,8 @@ extern "C" int vox_profile(vox_model* m, const float* d_x, int n, int t, int f, 
         tag |= (1 << 25) | (1 << 19);
       else if (o.type == 25)
         tag |= (1 << 29) | (1 << 18);
+      else if (o.type == 26)
+        tag |= (1 << 29) | (1 << 18) | (1 << 17);
       else if (o.type == 8)
         tag |= (o.cl.wco << 4) | (o.cl.wpx << 8) | (((o.cp.cinp + 31) / 32) << 16) | (1 << 20);
       else if (o.type == 0 || o.type == 5)
@@ -1709,12 +1716,12 @@ extern "C" int vox_plan_describe(vox_model* m, const float* d_x, int n, int t, i
   static const char* tn[] = {"igemm", "reduce", "pool", "avgpool", "convert", "igemm32", "bnrelu",
                              "win", "rr", "gemm", "chain", "stem", "bneck", "chainrows", "splits2",
                              "cvt16", "atttanh", "attpool", "gemmpipe", "gconv", "conv3pipe",
-                             "gemmwide", "s2fused", "conv3win", "chainfused", "conv3rw"};
+                             "gemmwide", "s2fused", "conv3win", "chainfused", "conv3rw", "conv3utt"};
   for (const Op& o : m->plan) {
     char line[256];
     const ConvParams& p = o.cp;
     if (o.type == 0 || o.type == 5 || o.type == 7 || o.type == 8 || o.type == 9 || o.type == 18 ||
-        o.type == 20 || o.type == 21 || o.type == 23 || o.type == 25)
+        o.type == 20 || o.type == 21 || o.type == 23 || o.type == 25 || o.type == 26)
       std::snprintf(line, sizeof(line),
                     "%s wco=%d wpx=%d s=%d N=%d H=%d W=%d Cin=%d Ho=%d Wo=%d Cout=%d k=%dx%d st=%d "
                     "g=%d flags=%d x2=%d pro=%d flops=%.4g bytes=%.4g\n",

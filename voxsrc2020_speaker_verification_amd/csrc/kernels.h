@@ -133,6 +133,9 @@ hipError_t launch_gemm_pipe(const ConvParams& p, int num_cu, int variant, hipStr
 // registers, the input window staged once per 128-pixel tile.
 int conv3_rw_ok(const ConvParams& p);
 hipError_t launch_conv3_rw(const ConvParams& p, int num_cu, hipStream_t s);
+// Utterance-band window 3x3 conv for the w = 192 stride-1 branches (conv3u.hip)
+int conv3_utt_ok(const ConvParams& p);
+hipError_t launch_conv3_utt(const ConvParams& p, int num_cu, hipStream_t s);
 int conv3_win_ok(const ConvParams& p);
 hipError_t launch_conv3_win(const ConvParams& p, int num_cu, hipStream_t s);
 // Wide-tile variant (gemm_wide.hip): 256 x BN tiles, BN = 256 (Cout % 256 == 0)
