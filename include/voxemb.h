@@ -142,6 +142,28 @@ int vox_sliding_cmn_device(const float* d_in, const int64_t* d_frame_off, int n_
 
 const char* vox_last_error(void);
 
+/* ---- layer-by-layer parity support (tests, not the extraction path) ------
+ * The plan at (n, t) for the device buffers (d_x, d_out) is a sequence of
+ * kernel launches; after launches [0, op_end) of tap i have run, `data` holds
+ * layer i's output (NHWC [n,h,w,c], row stride `ld` elements, dtype VOX_BF16 /
+ * VOX_FP32 = the model precision).  Layers are the oracle's boundaries
+ * (oracle/models_ref.py `layers`): the stem / first TDNN layer, every
+ * bottleneck / DPN block / TDNN layer; the remaining launches are pooling and
+ * the head.  vox_debug_taps returns the tap count (fills up to max_taps) and
+ * the number of launches of the whole plan in *n_ops;
+ * vox_debug_run_ops runs launches [op_begin, op_end) eagerly and synchronises;
+ * vox_debug_read copies device bytes to the host. */
+typedef struct vox_tap {
+  int op_end;
+  int n, h, w, c, ld;
+  int dtype;
+  const void* data;
+} vox_tap;
+int vox_debug_taps(vox_model* m, const float* d_x, int n, int t, int f, float* d_out,
+                   vox_tap* taps, int max_taps, int* n_ops);
+int vox_debug_run_ops(vox_model* m, int op_begin, int op_end, void* stream);
+int vox_debug_read(void* dst, const void* d_src, size_t bytes);
+
 /* ---- host-side Kaldi I/O (no Kaldi binaries needed) --------------------- */
 int vox_sliding_cmn(const float* in, int t, int f, int cmn_window, int center,
                     float* out);

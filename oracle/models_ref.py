@@ -1,15 +1,38 @@
-"""ORACLE (test infrastructure only) -- numpy fp32 restatement of the reference
-TF1 inference graph for the extraction hot path.
+"""ORACLE (test infrastructure only) -- numpy restatement of the reference
+TF1 inference graph for the extraction hot path, in two arithmetic modes.
 
 Only `tests/`, `__graft_entry__.smoke()` and `bench.py`'s cpu_baseline leg may
 import this module, and only as the checker / CPU baseline.  The product path
 (`voxsrc2020_speaker_verification_amd`) never imports it.
 
+Modes (the `precision` argument of `forward` / `layers`):
+  * "fp32": the reference's own arithmetic (float32 variables and activations,
+    models.py:191-197) -- the parity mode of the HIP library.
+  * "bf16": the same graph with activations rounded to bfloat16
+    (round-to-nearest-even) at exactly the points where the HIP library's bf16
+    mode stores them (north_star: conv contractions on bf16 MFMA, fp32
+    accumulation):
+      - the input features (the stem / first TDNN layer read bf16 values);
+      - conv weights (not BN statistics, not the fp32 head / attention weights);
+      - every conv output after its epilogue: Res2Net stem / 1x1a / 3x3
+        branch -> BN -> ReLU, the 1x1 projection -> BN, the 1x1c -> BN (+ the
+        shortcut, then ReLU, one rounding), TDNN conv -> ReLU -> BN, DPN
+        BN -> ReLU prologue of every conv input, DPN conv outputs, and the DPN
+        residual sum r + conv (one rounding);
+      - the Res2Net hierarchical addend z_k = x_k + y_{k-1} and the stride-2
+        average pool of the last split;
+      - stats pooling, attentive pooling and the head stay fp32 (they read the
+        bf16 block output).
+    BN is applied as (x - mean) * (1 / sqrt(var + eps)) in float32 with the
+    BN and residual additions as separate roundings, as TF and the kernels do.
+
 Parity status: TensorFlow is not installed and no frozen `.pb` exists in this
 pipeline, so the model forward is *parity unpinned* against TF itself.  It is
 re-derived from the reference source (cited per function below and in SURVEY.md
 Appendix A) and cross-checked against an independent torch-CPU implementation
-in `tests/test_oracle_models.py`.
+in `tests/test_oracle_models.py`.  The bf16 mode is pinned to the fp32 mode
+(identical with rounding disabled) and to an independent float64-accumulation
+run of itself (`tests/test_oracle_models.py`).
 
 Layout is NHWC throughout, H = time, W = frequency (2-D models, expand_dim=3) or
 W = 1, C = frequency (TDNN, expand_dim=2) -- tf_extract.py:32,
@@ -23,6 +46,40 @@ import numpy as np
 BN_EPS_4D = 1.001e-5   # fused BN clamps eps to >= 1.001e-5 (models.py:62-67)
 BN_EPS_2D = 1e-5       # 2-D head BNs are non-fused (models.py:20)
 STATS_EPS = 1e-5       # stats_pool epsilon (models.py:262)
+
+# float64 accumulation for every contraction (tests only: an independent
+# summation order for the bf16 mode's self-check); default float32 BLAS
+_ACC64 = False
+
+
+def bf16(a):
+    """Round float32 values to the nearest bfloat16 (ties to even), returned as
+    float32 holding the bf16 value (what a bf16 store + reload gives)."""
+    a = np.ascontiguousarray(a, np.float32)
+    u = a.view(np.uint32)
+    r = (u + (np.uint32(0x7FFF) + ((u >> np.uint32(16)) & np.uint32(1)))) & np.uint32(0xFFFF0000)
+    return r.view(np.float32)
+
+
+class _Q:
+    """Rounding points of one arithmetic mode (module docstring)."""
+
+    def __init__(self, precision):
+        if precision not in ("fp32", "bf16"):
+            raise ValueError(precision)
+        self.bf = precision == "bf16"
+
+    def act(self, x):
+        return bf16(x) if self.bf else np.asarray(x, np.float32)
+
+    def w(self, k):
+        return bf16(k) if self.bf else k
+
+
+def _mm(a, b):
+    if _ACC64:
+        return (a.astype(np.float64) @ b.astype(np.float64)).astype(np.float32)
+    return (a @ b).astype(np.float32)
 
 
 # --------------------------------------------------------------------------- ops
@@ -55,14 +112,17 @@ def conv2d(x, w, strides=(1, 1), dilations=(1, 1), pads=((0, 0), (0, 0)), groups
     outs = []
     for g in range(groups):
         xg = xp[..., g * cig:(g + 1) * cig]
-        taps = []
-        for ky in range(kh):
-            for kx in range(kw):
-                y0, x0 = ky * dh, kx * dw
-                taps.append(xg[:, y0:y0 + (Ho - 1) * sh + 1:sh, x0:x0 + (Wo - 1) * sw + 1:sw, :])
-        cols = np.stack(taps, axis=3).reshape(N * Ho * Wo, kh * kw * cig)
+        if kh == kw == 1 and sh == sw == 1:
+            cols = xg.reshape(N * Ho * Wo, cig)
+        else:
+            taps = []
+            for ky in range(kh):
+                for kx in range(kw):
+                    y0, x0 = ky * dh, kx * dw
+                    taps.append(xg[:, y0:y0 + (Ho - 1) * sh + 1:sh, x0:x0 + (Wo - 1) * sw + 1:sw, :])
+            cols = np.stack(taps, axis=3).reshape(N * Ho * Wo, kh * kw * cig)
         wg = w[..., g * cog:(g + 1) * cog].reshape(kh * kw * cig, cog)
-        outs.append((cols @ wg).reshape(N, Ho, Wo, cog))
+        outs.append(_mm(cols, wg).reshape(N, Ho, Wo, cog))
     return np.concatenate(outs, axis=3) if groups > 1 else outs[0]
 
 
@@ -176,30 +236,43 @@ class _Params:
         return self.i == len(self.items)
 
 
-def _head_tail(p, x):
+def _head_layer(p):
+    """stats already pooled + flattened -> BN(2-D) -> dense -> BN(2-D), fp32."""
     m1, v1 = p.bn()
-    x = batch_norm(x, m1, v1, BN_EPS_2D)
-    x = (x @ p.conv()).astype(np.float32)
+    dense = p.conv()
     m2, v2 = p.bn()
     assert p.done()
-    return batch_norm(x, m2, v2, BN_EPS_2D)
+
+    def f(x):
+        x = batch_norm(x, m1, v1, BN_EPS_2D)
+        x = _mm(x, dense)
+        return batch_norm(x, m2, v2, BN_EPS_2D)
+    return f
 
 
-def tdnn_forward(spec, tensors, x):
-    """tdnn_model.py:128-155 with conv_relu_bn_block :24-30.  x: [N,T,1,F]."""
+def tdnn_layers(spec, tensors, q):
+    """tdnn_model.py:128-155 with conv_relu_bn_block :24-30.  Layer 0 takes the
+    [N,T,F] features (expand_dim 2 -> [N,T,1,F], tf_extract.py:32)."""
     p = _Params(tensors)
-    for k, d in zip(spec["kernels"], spec["dilations"]):
-        w = p.conv()
-        x = conv2d_same(x, w, (1, 1), (d, 1))
-        x = relu(x)
+    out = []
+    for i, (k, d) in enumerate(zip(spec["kernels"], spec["dilations"])):
+        w = q.w(p.conv())
         m, v = p.bn()
-        x = batch_norm(x, m, v)
-    x = flatten_nhwc(stats_pool(x))
-    return _head_tail(p, x)
+
+        def f(x, w=w, d=d, m=m, v=v, first=(i == 0)):
+            if first:
+                x = q.act(np.asarray(x, np.float32)[:, :, None, :])
+            return q.act(batch_norm(relu(conv2d_same(x, w, (1, 1), (d, 1))), m, v))
+        out.append((f"tdnn{i}", f))
+    hd = _head_layer(p)
+    out.append(("pool+head", lambda x: hd(flatten_nhwc(stats_pool(x)))))
+    return out
 
 
-def res2net_split_conv(h, kernel, bns, stride, split, width):
-    """res2net_model.py:26-78 (hierarchical split-scale 3x3 conv)."""
+def res2net_split_conv(h, kernel, bns, stride, split, width, q=None):
+    """res2net_model.py:26-78 (hierarchical split-scale 3x3 conv); `h` is the
+    (rounded) 1x1a output, kernel the (rounded) [3,3,w,w*(split-1)] variable."""
+    q = q or _Q("fp32")
     if stride > 1:
         h = np.pad(h, ((0, 0), (1, 1), (1, 1), (0, 0)))       # fixed_padding(k=3)
     parts = [h[..., i * width:(i + 1) * width] for i in range(split)]
@@ -210,78 +283,109 @@ def res2net_split_conv(h, kernel, bns, stride, split, width):
             y = conv2d_same(inp, k)
         else:
             y = conv2d(inp, k, (stride, stride))                # VALID
-        return relu(batch_norm(y, *bn))
+        return q.act(relu(batch_norm(y, *bn)))
 
     outs = [cbr(parts[0], kernels[0], bns[0])]
     for idx in range(1, split - 1):
         inp = parts[idx]
         if stride == 1:
-            inp = inp + outs[idx - 1]
+            inp = q.act(inp + outs[idx - 1])
         outs.append(cbr(inp, kernels[idx], bns[idx]))
     if stride == 1:
         outs.append(parts[split - 1])
     else:
-        outs.append(avg_pool3x3s2_valid(parts[split - 1]))
+        outs.append(q.act(avg_pool3x3s2_valid(parts[split - 1])))
     return np.concatenate(outs, axis=3)
 
 
-def res2net_forward(spec, tensors, x):
+def res2net_layers(spec, tensors, q):
     """res2net_model.py:185-243 (v1 bottleneck :81-103, block_layer :106-136).
-    x: [N,T,F,1]."""
+    Layer 0 (the stem) takes the [N,T,F] features (expand_dim 3 -> [N,T,F,1])."""
     p = _Params(tensors)
     s = spec["split"]
-    x = conv2d_fixed_padding(x, p.conv(), 1)                 # :192-194
-    x = relu(batch_norm(x, *p.bn()))                         # :202-203
+    ws = q.w(p.conv())
+    bs = p.bn()
+
+    def stem(x):                                              # :192-203
+        x = q.act(np.asarray(x, np.float32)[..., None])
+        return q.act(relu(batch_norm(conv2d_fixed_padding(x, ws, 1), *bs)))
+    out = [("stem", stem)]
     for i, nblocks in enumerate(spec["block_sizes"]):
         w = spec["widths"][i]
         for b in range(nblocks):
             stride = spec["block_strides"][i] if b == 0 else 1
-            if b == 0:
-                sc = batch_norm(conv2d_fixed_padding(x, p.conv(), stride), *p.bn())
-            else:
-                sc = x
-            h = relu(batch_norm(conv2d_fixed_padding(x, p.conv(), 1), *p.bn()))
-            kern = p.conv()
+            proj = (q.w(p.conv()), p.bn()) if b == 0 else None
+            ka, bna = q.w(p.conv()), p.bn()
+            kern = q.w(p.conv())
             bns = [p.bn() for _ in range(s - 1)]
-            h = res2net_split_conv(h, kern, bns, stride, s, w)
-            h = batch_norm(conv2d_fixed_padding(h, p.conv(), 1), *p.bn())
-            x = relu(h + sc)
+            kc, bnc = q.w(p.conv()), p.bn()
+
+            def block(x, stride=stride, proj=proj, ka=ka, bna=bna, kern=kern, bns=bns, kc=kc,
+                      bnc=bnc, w=w):
+                if proj is not None:                          # projection_shortcut
+                    sc = q.act(batch_norm(conv2d_fixed_padding(x, proj[0], stride), *proj[1]))
+                else:
+                    sc = x
+                h = q.act(relu(batch_norm(conv2d_fixed_padding(x, ka, 1), *bna)))
+                h = res2net_split_conv(h, kern, bns, stride, s, w, q)
+                h = batch_norm(conv2d_fixed_padding(h, kc, 1), *bnc)
+                return q.act(relu(h + sc))
+            out.append((f"layer{i + 1}.block{b}", block))
     if spec.get("pool") == "att":                            # res2net_model.py:229
-        x = flatten_nhwc(att_stats_pool(x, p.conv(), p.conv()))
+        k1, k2 = p.conv(), p.conv()
+        pool = lambda x: flatten_nhwc(att_stats_pool(x, k1, k2))
     else:
-        x = flatten_nhwc(stats_pool(x))
-    return _head_tail(p, x)
+        pool = lambda x: flatten_nhwc(stats_pool(x))
+    hd = _head_layer(p)
+    out.append(("pool+head", lambda x: hd(pool(x))))
+    return out
 
 
-def dpn_forward(spec, tensors, x):
+def dpn_layers(spec, tensors, q):
     """dpn_model.py:111-168 (dual_path_block :57-87, bn_relu_conv :40-45).
-    x: [N,T,F,1]."""
+    Each block maps the concatenated state [res | dense] (a channel prefix of
+    one stage buffer in the HIP plan) to the next state."""
     from voxsrc2020_speaker_verification_amd.archs import dpn_stage_params  # spec helper only
     p = _Params(tensors)
     G = spec["cardinality"]
 
-    def bn_relu(t):
-        return relu(batch_norm(t, *p.bn()))
+    def bnrelu_args():
+        return p.bn()
 
-    x = relu(batch_norm(conv2d_same(x, p.conv()), *p.bn()))    # conv_bn_relu :32-37
-    state = x
-    for bw, r, inc, blocks, ptype in dpn_stage_params(spec):
+    def bn_relu(t, bn):
+        return q.act(relu(batch_norm(t, *bn)))
+
+    ws = q.w(p.conv())
+    bs = p.bn()
+
+    def stem(x):                                              # conv_bn_relu :32-37
+        x = q.act(np.asarray(x, np.float32)[..., None])
+        return q.act(relu(batch_norm(conv2d_same(x, ws), *bs)))
+    out = [("stem", stem)]
+    for si, (bw, r, inc, blocks, ptype) in enumerate(dpn_stage_params(spec)):
         for b in range(blocks):
             stride = 2 if (b == 0 and ptype == "downsampled") else 1
-            if b == 0:
-                inp = state if not isinstance(state, list) else np.concatenate(state, axis=3)
-                proj = conv2d_same(bn_relu(inp), p.conv(), (stride, stride))
-                r0, d0 = proj[..., :bw], proj[..., bw:]
-            else:
-                r0, d0 = state
-                inp = np.concatenate(state, axis=3)
-            h = conv2d_same(bn_relu(inp), p.conv())
-            h = conv2d_same(bn_relu(h), p.conv(), (stride, stride), groups=G)
-            h = conv2d_same(bn_relu(h), p.conv())
-            state = [r0 + h[..., :bw], np.concatenate([d0, h[..., bw:]], axis=3)]
-    x = bn_relu(np.concatenate(state, axis=3))                  # concat_bn_relu :24-29
-    x = flatten_nhwc(stats_pool(x))
-    return _head_tail(p, x)
+            pr = (bnrelu_args(), q.w(p.conv())) if b == 0 else None
+            c1 = (bnrelu_args(), q.w(p.conv()))
+            c2 = (bnrelu_args(), q.w(p.conv()))
+            c3 = (bnrelu_args(), q.w(p.conv()))
+
+            def block(inp, stride=stride, pr=pr, c1=c1, c2=c2, c3=c3, bw=bw):
+                if pr is not None:
+                    proj = q.act(conv2d_same(bn_relu(inp, pr[0]), pr[1], (stride, stride)))
+                    r0, d0 = proj[..., :bw], proj[..., bw:]
+                else:
+                    r0, d0 = inp[..., :bw], inp[..., bw:]
+                h = q.act(conv2d_same(bn_relu(inp, c1[0]), c1[1]))
+                h = q.act(conv2d_same(bn_relu(h, c2[0]), c2[1], (stride, stride), groups=G))
+                h = conv2d_same(bn_relu(h, c3[0]), c3[1])
+                return np.concatenate([q.act(r0 + h[..., :bw]), d0, q.act(h[..., bw:])], axis=3)
+            out.append((f"stage{si + 1}.block{b}", block))
+    fb = p.bn()
+    hd = _head_layer(p)
+    # concat_bn_relu :24-29, stats pool, head
+    out.append(("pool+head", lambda x: hd(flatten_nhwc(stats_pool(bn_relu(x, fb))))))
+    return out
 
 
 def _eps_from(spec):
@@ -290,24 +394,37 @@ def _eps_from(spec):
     BN_EPS_2D = float(spec.get("bn_eps_2d", 1e-5))
 
 
-def forward(spec, tensors, feats):
-    """One `sess.run(outputs, {inputs: x})` (tf_extract.py:108).
-
-    feats: [N, T, F] float32 (post-CMN FBANK).  The expand_dim rule of
-    tf_extract.py:32 is applied here: TDNN -> [N,T,1,F], 2-D -> [N,T,F,1]."""
-    feats = np.asarray(feats, np.float32)
+def layers(spec, tensors, precision="fp32"):
+    """The forward as [(name, fn)]: fn maps one layer's input to its output;
+    the first takes the [N,T,F] features, the last ("pool+head") returns the
+    [N,D] embeddings.  The boundaries are the block outputs the HIP plan
+    exposes as taps (vox_debug_taps), so a test can feed layer i the GPU's own
+    output of layer i-1 (teacher forcing)."""
     _eps_from(spec)
+    q = _Q(precision)
     fam = spec["family"]
     if fam == "tdnn":
-        return tdnn_forward(spec, tensors, feats[:, :, None, :])
+        return tdnn_layers(spec, tensors, q)
     if fam == "res2net":
-        return res2net_forward(spec, tensors, feats[..., None])
+        return res2net_layers(spec, tensors, q)
     if fam == "dpn":
-        return dpn_forward(spec, tensors, feats[..., None])
+        return dpn_layers(spec, tensors, q)
     raise ValueError(fam)
 
 
-def embed_utterance(spec, tensors, feat, max_frames=1000):
+def forward(spec, tensors, feats, precision="fp32"):
+    """One `sess.run(outputs, {inputs: x})` (tf_extract.py:108).
+
+    feats: [N, T, F] float32 (post-CMN FBANK).  The expand_dim rule of
+    tf_extract.py:32 is applied by the first layer: TDNN -> [N,T,1,F],
+    2-D -> [N,T,F,1]."""
+    x = np.asarray(feats, np.float32)
+    for _, f in layers(spec, tensors, precision):
+        x = f(x)
+    return x
+
+
+def embed_utterance(spec, tensors, feat, max_frames=1000, precision="fp32"):
     """tf_extract.py:96-111 chunk rule: n = 1 + (T-25)//1000; chunk i has
     length 1000 if (i+1)*1000 <= T else T-1000*i; length-weighted average.
     T < 25 gives 0 chunks and a ZeroDivisionError, as in the reference."""
@@ -316,7 +433,7 @@ def embed_utterance(spec, tensors, feat, max_frames=1000):
     vals, lens = [], []
     for i in range(n):
         L = max_frames if (i + 1) * max_frames <= T else T - i * max_frames
-        e = forward(spec, tensors, feat[None, i * max_frames:i * max_frames + L])
+        e = forward(spec, tensors, feat[None, i * max_frames:i * max_frames + L], precision)
         vals.append(e * L)
         lens.append(L)
     return (sum(vals) / sum(lens))[0]

@@ -11,7 +11,12 @@ What is pinned to what:
     read_mat_ark :367).
   * snorm.py (tensorflow/snorm.py)        -> l2norm / read_xvector / cohort
     speaker means / cosine trial scores / top-400 cohort mean,std / AS-norm
-    (:23-131) on seeded synthetic embeddings.
+    (:23-131) on seeded synthetic embeddings; the `--weight_matrix` cohort
+    (get_projection_weight :77-80) on a projection matrix this script pickles
+    itself (its own file, loaded by the reference function as snorm.py does).
+  * export_projection_weight.py:28-35 (imports TensorFlow, so not importable
+    here): its post-read arithmetic -- swapaxes(-1,-2), reshape(-1, last),
+    row l2norm with snorm's l2norm -- restated on a seeded head variable.
   * eer_minDCF.py                          -> compute_eer_and_min_dcf (:43-64).
   * utt2id.py                              -> read_spk / read_utt2spk (:20-41)
     and the argv pairing loop of its __main__ (:44-53), restated verbatim.
@@ -140,6 +145,37 @@ def scoring_fixtures():
              test_keys=np.array(keys))
 
 
+def projection_fixtures():
+    """sc-CM style head variable [2, D, nspk] (two centres per speaker, kernel
+    [..., in, out]) ->
+    export_projection_weight.load's arithmetic -> pickle -> snorm's
+    get_projection_weight -> top-400 cohort stats / AS-norm of the golden
+    test set and trials."""
+    rng = np.random.default_rng(31)
+    D, nspk = 32, 230
+    var = rng.standard_normal((2, D, nspk)).astype(np.float32)
+    # export_projection_weight.py:28-35 (restated: the module imports TensorFlow)
+    weight = np.swapaxes(var, -1, -2)
+    weight = np.reshape(weight, (-1, weight.shape[-1]))
+    weight = snorm.l2norm(weight, axis=1)
+    fd, pkl = tempfile.mkstemp(suffix=".pkl")
+    os.close(fd)
+    import pickle
+    with open(pkl, "wb") as f:
+        pickle.dump(weight, f)                         # this script's own file
+    coh = snorm.get_projection_weight(pkl)             # snorm.py:77-80
+    tx = snorm.read_xvector(os.path.join(OUT, "snorm_test.ark"))
+    cos = snorm.get_cosine_score(tx, os.path.join(OUT, "snorm_trials.txt"))
+    mean, std = snorm.get_cohort_mean_std(tx, coh)
+    asn = snorm.get_asnorm1_score(mean, std, cos)
+    keys = list(tx)
+    np.save(os.path.join(OUT, "proj_head_var.npy"), var)
+    np.savez(os.path.join(OUT, "proj_expected.npz"), weight=weight,
+             cohort=np.array(list(coh.values())), mean=np.array([mean[k] for k in keys]),
+             std=np.array([std[k] for k in keys]),
+             asnorm=np.array([s for _, _, s in asn], np.float64), test_keys=np.array(keys))
+
+
 def eer_fixtures():
     rng = np.random.default_rng(11)
     cases = {}
@@ -208,6 +244,7 @@ def split_fixtures():
 if __name__ == "__main__":
     kaldi_fixtures()
     scoring_fixtures()
+    projection_fixtures()
     eer_fixtures()
     utt2id_fixtures()
     split_fixtures()

@@ -97,3 +97,41 @@ def test_dp_extract_rank_failure_aborts_all(tmp_path):
     mp.spawn(_failing_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
     got = [open(tmp_path / f"r{r}").read() for r in range(world)]
     assert got == ["peer", "own", "peer"]
+
+
+def _resume_worker(rank, world, port, outdir, n_utts):
+    import torch.distributed as dist
+    from voxsrc2020_speaker_verification_amd import dp_extract
+    from voxsrc2020_speaker_verification_amd.partition import shard
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    feats, items = _items(n_utts)
+
+    def counted(x):   # marks that this rank ran the extractor
+        with open(os.path.join(outdir, f"ran{rank}"), "a") as f:
+            f.write("x")
+        return _fake_embed(x)
+    dp_extract.run(rank, world, items, counted, 8, os.path.join(outdir, "xvector"), batch=3,
+                   resume=True, shard_keys=lambda r, w: [k for k, _ in shard(feats, r, w)])
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_dp_extract_resume_skips_finished_shards(tmp_path):
+    """SURVEY §5 resume: a second run with resume=True reuses the ranks whose
+    xvector.<i>.ark/.scp hold their whole shard and recomputes the others (here
+    rank 2's ark was cut short, as by a crash); the merged output is identical."""
+    import torch.multiprocessing as mp
+    world, n = 3, 10
+    mp.spawn(_resume_worker, args=(world, _free_port(), str(tmp_path), n), nprocs=world, join=True)
+    first = open(tmp_path / "xvector.ark", "rb").read()
+    assert sorted(p.name for p in tmp_path.glob("ran*")) == ["ran0", "ran1", "ran2"]
+    for p in tmp_path.glob("ran*"):
+        p.unlink()
+    ark2 = tmp_path / "xvector.3.ark"
+    ark2.write_bytes(ark2.read_bytes()[:-7])     # truncated record
+    (tmp_path / "xvector.ark").unlink()
+    mp.spawn(_resume_worker, args=(world, _free_port(), str(tmp_path), n), nprocs=world, join=True)
+    assert sorted(p.name for p in tmp_path.glob("ran*")) == ["ran2"]
+    assert open(tmp_path / "xvector.ark", "rb").read() == first
+    assert not list(tmp_path.glob("*.part*"))

@@ -487,3 +487,22 @@ def test_conv3_win_bitwise_pipe(weights, name, F, T, N, monkeypatch):
         ref = ex.run(x)
         assert not any(l.startswith("conv3win") for l in ex.describe(torch.from_numpy(x).cuda()))
     assert np.array_equal(got, ref)
+
+
+def test_run_device_new_buffers_without_sync(weights):
+    """Back-to-back run_device calls on fresh input/output tensors with no
+    synchronisation in between: each call rebuilds the plan (new pointers)
+    while the previous graph replay may still run; the rebuild waits for it
+    (api.cpp build_plan), so every result equals the synchronous host path."""
+    import torch
+    from voxsrc2020_speaker_verification_amd import synth
+    spec, t, blob = weights("res2net50_w24_s4_c32", 80)
+    xs = [synth.make_features(6, 200, 80, seed=s) for s in (61, 62, 63)]
+    with _extractor(blob, "bf16") as ex:
+        outs = [ex.run_device(torch.from_numpy(x).cuda()) for x in xs]
+        outs.append(ex.run_device(torch.from_numpy(xs[0]).cuda()))
+        torch.cuda.synchronize()
+        got = [o.cpu().numpy() for o in outs]
+        ref = [ex.run(x) for x in xs]
+    for g, r in zip(got, ref + [ref[0]]):
+        assert np.array_equal(g, r)

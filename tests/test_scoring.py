@@ -77,3 +77,41 @@ def test_cli_mirrors(tmp_path, capsys):
     eer_minDCF.main(["--trial", os.path.join(G, "snorm_trials.txt"), "--score", str(cos)])
     out = capsys.readouterr().out
     assert out.startswith("EER is ") and "minDCF is " in out
+
+
+def test_projection_weight_cohort_matches_reference(tmp_path):
+    """export_projection_weight.py:28-35's arithmetic and the
+    `--weight_matrix` cohort of snorm.py:77-80,171-172 against golden values the
+    reference's snorm functions produced (tests/golden/make_golden.py
+    projection_fixtures): projection matrix, cohort rows, top-400 statistics
+    and AS-norm scores, through the library functions and the CLIs."""
+    from voxsrc2020_speaker_verification_amd import export_projection_weight as E
+    from voxsrc2020_speaker_verification_amd import scoring as S
+    from voxsrc2020_speaker_verification_amd import snorm
+    exp = np.load(os.path.join(G, "proj_expected.npz"))
+    var = np.load(os.path.join(G, "proj_head_var.npy"))
+    w = E.projection_weight(var)
+    assert w.shape == (2 * var.shape[-1], var.shape[-2])
+    assert np.array_equal(w, exp["weight"])
+    coh = S.projection_cohort(w)
+    assert list(coh) == list(range(len(w)))
+    assert np.array_equal(np.array(list(coh.values())), exp["cohort"])
+    tx = S.read_xvector(os.path.join(G, "snorm_test.ark"))
+    m, s = S.cohort_mean_std(tx, coh)
+    keys = list(exp["test_keys"])
+    assert np.array_equal(np.array([m[k] for k in keys]), exp["mean"])
+    assert np.array_equal(np.array([s[k] for k in keys]), exp["std"])
+    cos = S.cosine_scores(tx, os.path.join(G, "snorm_trials.txt"))
+    asn = S.asnorm_scores(m, s, cos)
+    assert np.array_equal(np.array([v for *_, v in asn], np.float64), exp["asnorm"])
+    # the two command lines: export -> .npy -> snorm --weight_matrix
+    np.save(tmp_path / "var.npy", var)
+    E.main(["--input_npy", str(tmp_path / "var.npy"), "--output_weight", str(tmp_path / "w.npy")])
+    assert np.array_equal(np.load(tmp_path / "w.npy"), exp["weight"])
+    cos_f, asn_f = tmp_path / "cos.txt", tmp_path / "asn.txt"
+    snorm.main(["--trial", os.path.join(G, "snorm_trials.txt"),
+                "--test_ark", os.path.join(G, "snorm_test.ark"), "--cosine_score", str(cos_f),
+                "--weight_matrix", str(tmp_path / "w.npy"), "--snorm_score", str(asn_f)])
+    got = [l.split()[2] for l in open(asn_f)]
+    # the reference prints numpy float32 scalars: the same text
+    assert got == [str(np.float32(v)) for v in exp["asnorm"]]

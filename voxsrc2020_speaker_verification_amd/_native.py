@@ -37,6 +37,12 @@ class FbankOpts(C.Structure):
                 ("seed", C.c_uint64)]
 
 
+class Tap(C.Structure):
+    """vox_tap (include/voxemb.h): one layer output of the plan."""
+    _fields_ = [("op_end", C.c_int), ("n", C.c_int), ("h", C.c_int), ("w", C.c_int),
+                ("c", C.c_int), ("ld", C.c_int), ("dtype", C.c_int), ("data", C.c_void_p)]
+
+
 _FO = C.POINTER(FbankOpts)
 _SIGS = [
     ("vox_load", C.c_int, [C.c_char_p, C.c_int, C.c_int, C.POINTER(_P)]),
@@ -59,6 +65,10 @@ _SIGS = [
     ("vox_asnorm_stats", C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int,
                                    C.c_void_p, C.c_void_p, C.c_void_p]),
     ("vox_last_error", C.c_char_p, []),
+    ("vox_debug_taps", C.c_int, [_P, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                                 C.POINTER(Tap), C.c_int, C.POINTER(C.c_int)]),
+    ("vox_debug_run_ops", C.c_int, [_P, C.c_int, C.c_int, _P]),
+    ("vox_debug_read", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
     ("vox_sliding_cmn", C.c_int, [_F, C.c_int, C.c_int, C.c_int, C.c_int, _F]),
     ("vox_mat_shape", C.c_int, [C.c_char_p, C.c_int64, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     ("vox_read_mat", C.c_int, [C.c_char_p, C.c_int64, _F, C.c_int, C.c_int]),

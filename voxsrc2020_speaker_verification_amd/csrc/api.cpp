@@ -198,6 +198,14 @@ struct Op {
 
 enum Slot { S_IN, S_X0, S_X1, S_A, S_B, S_SC, S_POOL, S_PART, S_NSLOTS };
 
+// A layer output the plan exposes for layer-by-layer checks (vox_debug_taps):
+// after ops [0, op_end) have run, `p` holds that layer's NHWC output.
+struct Tap {
+  int op_end;
+  const void* p;
+  int n, h, w, c, ld;
+};
+
 struct vox_model {
   int device = 0;
   DType dt = BF16;
@@ -218,6 +226,10 @@ struct vox_model {
   const float* plan_x = nullptr;
   float* plan_out = nullptr;
   std::vector<Op> plan;
+  std::vector<Tap> taps;       // layer boundaries of the plan (debug / parity tests)
+  // completion of the last launch of the plan: waited for before a rebuild
+  // destroys the graph exec or reallocates the slots the launch still uses
+  hipEvent_t done = nullptr;
   // the plan's launches captured once into a hipGraph and replayed per call
   // (VOXEMB_NO_GRAPH=1: eager launches); rebuilt with the plan
   bool use_graph = true;
@@ -559,6 +571,9 @@ struct Builder {
     m->slot_need[s] = std::max(m->slot_need[s], bytes);
     return dry ? nullptr : (char*)m->slots[s].p;
   }
+  void tap(const void* p, int n, int h, int w, int c, int ld) {
+    m->taps.push_back(Tap{(int)ops->size(), p, n, h, w, c, ld});
+  }
 };
 
 struct Act {  // an NHWC activation view
@@ -884,6 +899,7 @@ static int build_tdnn(Builder& B, const float* x, int n, int t, float* out) {
     emit_conv(B, cw, a, nullptr, 0, 1, 1, d, 1, ph, 0, t, 1, y, cw.cout,
               EPI_PRE_RELU | EPI_AFFINE);
     a = Act{y, cw.cout, n, t, 1, cw.cout};
+    B.tap(y, n, t, 1, cw.cout, cw.cout);
   }
   float* pooled = (float*)B.base(S_POOL, (size_t)n * 2 * a.C * 4);
   emit_pool(B, a, pooled, m->head_bn1);
@@ -905,6 +921,7 @@ static int build_res2net(Builder& B, const float* x, int n, int t, float* out) {
   void* y = B.base(cur_s, (size_t)n * H * W * stem.cout * es);
   emit_stem(B, stem, x, n, H, W, y);  // res2net_model.py:192-203, SAME pad 1
   Act cur{y, stem.cout, n, H, W, stem.cout};
+  B.tap(y, n, H, W, stem.cout, stem.cout);
   for (size_t st = 0; st < blocks.size(); ++st) {
     const int w = widths[st];
     const int sw = s * w;
@@ -963,6 +980,7 @@ static int build_res2net(Builder& B, const float* x, int n, int t, float* out) {
           B.ops->push_back(op);
           ci = base + s + 1;
           cur = Act{yo, C, n, H, W, C};
+          B.tap(yo, n, H, W, C, C);
           std::swap(cur_s, nxt_s);
           continue;
         }
@@ -1251,6 +1269,7 @@ static int build_res2net(Builder& B, const float* x, int n, int t, float* out) {
       emit_conv(B, c1c, bin, nullptr, 0, 1, 1, 1, 1, 0, 0, Ho, Wo, yo, c1c.cout,
                 EPI_AFFINE | EPI_RES | EPI_RELU, shortcut, ld_sc);  // :98-101
       cur = Act{yo, c1c.cout, n, Ho, Wo, c1c.cout};
+      B.tap(yo, n, Ho, Wo, c1c.cout, c1c.cout);
       std::swap(cur_s, nxt_s);
       H = Ho;
       W = Wo;
@@ -1284,6 +1303,7 @@ static int build_dpn(Builder& B, const float* x, int n, int t, float* out) {
   void* y = B.base(S_SC, (size_t)n * H * W * stem.cout * es);
   emit_stem(B, stem, x, n, H, W, y);  // conv_bn_relu, SAME
   Act cur{y, stem.cout, n, H, W, stem.cout};
+  B.tap(y, n, H, W, stem.cout, stem.cout);
   for (size_t st = 0; st < ksec.size(); ++st) {
     const int bw = bw0 << st;
     const int r = kr * bw / bw0;
@@ -1350,6 +1370,7 @@ static int build_dpn(Builder& B, const float* x, int n, int t, float* out) {
                 EPI_RES, S, ctot, S ? S + (size_t)(bw + dense) * es : nullptr, ctot, bw,
                 (const float*)b3.mean->p, (const float*)b3.inv->p);
       dense += inc;
+      B.tap(S, n, Ho, Wo, bw + dense, ctot);
     }
     cur = Act{S, ctot, n, Ho, Wo, bw + dense};
     H = Ho;
@@ -1377,11 +1398,16 @@ static int build_plan(vox_model* m, const float* x, int n, int t, float* out) {
   auto run = [&](bool dry) -> int {
     Builder B{m, dry, &m->plan};
     m->plan.clear();
+    m->taps.clear();
     if (m->family == "tdnn") return build_tdnn(B, x, n, t, out);
     if (m->family == "res2net") return build_res2net(B, x, n, t, out);
     if (m->family == "dpn") return build_dpn(B, x, n, t, out);
     return fail(VOX_EINVAL, "unknown family");
   };
+  // the previous plan's last launch may still be running on a caller's stream:
+  // its graph exec (and the kernel arguments HIP keeps with it) and the slots
+  // it reads and writes must outlive it
+  if (m->done) HIPCHK(hipEventSynchronize(m->done));
   if (m->graph_exec) {
     (void)hipGraphExecDestroy(m->graph_exec);
     m->graph_exec = nullptr;
@@ -1514,6 +1540,7 @@ extern "C" int vox_load_blob(const void* blob, size_t nbytes, int device, int pr
   if (const char* e = std::getenv("VOXEMB_RR_WCO")) m->rr_wco = std::atoi(e);
   if ((rc = load_weights(m.get(), ts))) return rc;
   HIPCHK(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking));
+  HIPCHK(hipEventCreateWithFlags(&m->done, hipEventDisableTiming));
   *out = m.release();
   return VOX_OK;
 }
@@ -1535,6 +1562,7 @@ extern "C" void vox_free(vox_model* m) {
   }
   (void)hipDeviceSynchronize();   // replays launched on callers' streams
   if (m->graph_exec) (void)hipGraphExecDestroy(m->graph_exec);
+  if (m->done) (void)hipEventDestroy(m->done);
   delete m;
 }
 
@@ -1572,11 +1600,14 @@ extern "C" int vox_embed_device(vox_model* m, const float* d_x, int n, int t, in
       m->use_graph = false;
     }
   }
+  // calls on different streams share the slots: order after the previous launch
+  HIPCHK(hipStreamWaitEvent(s, m->done, 0));
   if (m->use_graph && m->graph_exec) {
     HIPCHK(hipGraphLaunch(m->graph_exec, s));
-    return VOX_OK;
+  } else {
+    for (const Op& op : m->plan) HIPCHK(run_op(m, op, s));
   }
-  for (const Op& op : m->plan) HIPCHK(run_op(m, op, s));
+  HIPCHK(hipEventRecord(m->done, s));
   return VOX_OK;
 }
 
@@ -1762,6 +1793,46 @@ extern "C" int vox_plan_describe(vox_model* m, const float* d_x, int n, int t, i
     buf[cap - 1] = 0;
   }
   return (int)out.size() + 1;
+}
+
+// ---- layer-by-layer parity support (tests/test_bf16_oracle.py) -------------
+extern "C" int vox_debug_taps(vox_model* m, const float* d_x, int n, int t, int f, float* d_out,
+                              vox_tap* taps, int max_taps, int* n_ops) {
+  if (!m || !d_x || !d_out) return fail(VOX_EINVAL, "null argument");
+  int rc = check_shape(m, n, t, f);
+  if (rc) return rc;
+  HIPCHK(hipSetDevice(m->device));
+  if ((rc = ensure_plan(m, d_x, n, t, d_out))) return rc;
+  const int nt = (int)m->taps.size();
+  if (n_ops) *n_ops = (int)m->plan.size();
+  for (int i = 0; i < nt && i < max_taps && taps; ++i) {
+    const Tap& a = m->taps[i];
+    taps[i].op_end = a.op_end;
+    taps[i].n = a.n; taps[i].h = a.h; taps[i].w = a.w; taps[i].c = a.c; taps[i].ld = a.ld;
+    taps[i].dtype = m->dt == BF16 ? VOX_BF16 : VOX_FP32;
+    taps[i].data = a.p;
+  }
+  return nt;
+}
+
+extern "C" int vox_debug_run_ops(vox_model* m, int op_begin, int op_end, void* stream) {
+  if (!m) return fail(VOX_EINVAL, "null argument");
+  const int nops = (int)m->plan.size();
+  if (op_begin < 0 || op_end > nops || op_begin > op_end)
+    return fail(VOX_EINVAL, "op range outside the plan");
+  HIPCHK(hipSetDevice(m->device));
+  hipStream_t s = stream ? (hipStream_t)stream : m->stream;
+  HIPCHK(hipStreamWaitEvent(s, m->done, 0));
+  for (int i = op_begin; i < op_end; ++i) HIPCHK(run_op(m, m->plan[i], s));
+  HIPCHK(hipEventRecord(m->done, s));
+  HIPCHK(hipStreamSynchronize(s));
+  return VOX_OK;
+}
+
+extern "C" int vox_debug_read(void* dst, const void* d_src, size_t bytes) {
+  if (!dst || !d_src) return fail(VOX_EINVAL, "null argument");
+  HIPCHK(hipMemcpy(dst, d_src, bytes, hipMemcpyDeviceToHost));
+  return VOX_OK;
 }
 
 extern "C" int vox_stats_pool_device(const void* d_x, int dtype, int n, int h, int w, int c,

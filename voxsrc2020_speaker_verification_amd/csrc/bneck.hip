@@ -403,6 +403,16 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
         epi(a0, a1, __builtin_bit_cast(bf16x8, res[j]), px);
         if (two) epi(c0, c1, __builtin_bit_cast(bf16x8, res[(j + 1) < PT ? j + 1 : j]), px + 16);
       }
+    } else if (is_c) {
+      // row c is outside the segment: the residual set requested two steps ago
+      // is not consumed, but load_res below reuses its registers.  Retire it
+      // first on this path too -- otherwise those registers are dead to the
+      // compiler while the loads are in flight, it builds the next addresses in
+      // them, and the late data (the zero line at the segment start) lands on
+      // an address: the illegal-address fault of the one-step variant (9c1d9bf)
+      vm_wait(t < 2 ? 0 : 2 * K::IREG + PT + ns_prev + 7 * nst);
+#pragma unroll
+      for (int j = 0; j < PT; ++j) vm_launder(res[j]);
     }
     if (!(q.dbg & 8)) load_res(P, c + 2);
     stamp(t, 1);
@@ -494,6 +504,12 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
     step(P0{}, t);
     if (t + 1 < steps) step(P1{}, t + 1);
   }
+  // the last prefetches (rows past the segment) retire before the wave ends
+  vm_wait(0);
+#pragma unroll
+  for (int i = 0; i < K::IREG; ++i) { vm_launder(inr[0][i]); vm_launder(inr[1][i]); }
+#pragma unroll
+  for (int j = 0; j < PT; ++j) { vm_launder(resb[0][j]); vm_launder(resb[1][j]); }
 }
 
 template <int CI, int C, int WID, int S, int PT>

@@ -61,21 +61,52 @@ def rank_failures(failed, device=None, group=None):
     return [r for r, f in enumerate(flags) if int(f.item())]
 
 
+def completed_shard(wspec, rank, keys, dim):
+    """The embeddings of rank's shard if `<wspec>.<rank+1>.ark/.scp` already
+    hold exactly `keys` (in order) as dim-D vectors, else None.  The pair is
+    written atomically (VectorWriter(atomic=True)), so a shard interrupted
+    mid-write is recomputed, never half-reused."""
+    from .kaldi import read_vec_flt_ark
+    base = f"{wspec}.{rank + 1}"
+    if not (os.path.exists(base + ".ark") and os.path.exists(base + ".scp")):
+        return None
+    try:
+        with open(base + ".scp") as f:
+            if [ln.split()[0] for ln in f if ln.strip()] != list(keys):
+                return None
+        got = list(read_vec_flt_ark(base + ".ark"))
+    except (OSError, ValueError, IndexError):
+        return None
+    if [k for k, _ in got] != list(keys) or any(np.shape(v) != (dim,) for _, v in got):
+        return None
+    return (np.stack([v for _, v in got]).astype(np.float32) if got
+            else np.zeros((0, dim), np.float32))
+
+
 def run(rank, world, scp_items, embed_fn, dim, wspec, shard_file=None, batch=64,
-        device=None, write_per_rank=True, cohort_spk2utt=None):
+        device=None, write_per_rank=True, cohort_spk2utt=None, resume=False, shard_keys=None):
     """The per-rank body (also used by the gloo tests with a fake embedder).
     scp_items: full list of (key, feat) is NOT required -- each rank only
     decodes its own shard: `scp_items` is a callable(rank, world) -> list of
-    (key, [T,F] features)."""
+    (key, [T,F] features).  resume: a rank whose per-rank ark/scp already hold
+    its shard (`shard_keys(rank, world)` -> keys, without decoding features)
+    reuses them -- the reference's per-shard processes are restartable one by
+    one in the same way (eval_inference_model.sh:29-36)."""
     from .extract import embed_utterances, write_vectors
     err = None
     try:
-        feats = scp_items(rank, world)
-        emb = (embed_utterances(feats, embed_fn, dim, batch) if feats
-               else np.zeros((0, dim), np.float32))
-        keys = [k for k, _ in feats]
-        if write_per_rank and wspec:
-            write_vectors(f"{wspec}.{rank + 1}", keys, emb)   # xvector.<i>.ark as the reference
+        emb = None
+        if resume and wspec and shard_keys is not None:
+            keys = list(shard_keys(rank, world))
+            emb = completed_shard(wspec, rank, keys, dim)
+        if emb is None:
+            feats = scp_items(rank, world)
+            emb = (embed_utterances(feats, embed_fn, dim, batch) if feats
+                   else np.zeros((0, dim), np.float32))
+            keys = [k for k, _ in feats]
+            if write_per_rank and wspec:
+                # xvector.<i>.ark as the reference; atomic for --resume
+                write_vectors(f"{wspec}.{rank + 1}", keys, emb, atomic=True)
     except Exception as e:   # e.g. ZeroDivisionError for a < 25-frame utterance
         err = e
     # every rank learns whether any shard failed BEFORE the gathers, so no rank
@@ -109,6 +140,8 @@ def main(argv=None):
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--cohort-spk2utt", default=None)
+    ap.add_argument("--resume", action="store_true",
+                    help="reuse per-rank xvector.<i>.ark/.scp that already hold the rank's shard")
     a = ap.parse_args(argv)
 
     import torch
@@ -139,9 +172,16 @@ def main(argv=None):
             out.append((key, sliding_cmn(m)))
         return out
 
+    def keys(r, w):
+        from .kaldi import read_scp
+        if a.pre_split:
+            return [k for k, _ in read_scp(f"{a.rspec}.{r + 1}.scp")]
+        return [k for k, _ in shard(read_scp(a.rspec + ".scp"), r, w)]
+
     with Extractor(a.pb_file, device=local, precision=a.precision) as ex:
         run(rank, world, items, ex.run, ex.dim, a.wspec, batch=a.batch,
-            device=torch.device("cuda", local), cohort_spk2utt=a.cohort_spk2utt)
+            device=torch.device("cuda", local), cohort_spk2utt=a.cohort_spk2utt,
+            resume=a.resume, shard_keys=keys)
     dist.barrier()
     dist.destroy_process_group()
     return 0

@@ -65,9 +65,9 @@ def extract_scp(scp_path, embed_batch, dim, batch=64, cmn=True):
     return [k for k, _ in feats], embed_utterances(feats, embed_batch, dim, batch)
 
 
-def write_vectors(base, keys, emb):
+def write_vectors(base, keys, emb, atomic=False):
     from .kaldi import VectorWriter
-    with VectorWriter(base) as w:
+    with VectorWriter(base, atomic=atomic) as w:
         for k, v in zip(keys, emb):
             w.write(k, v)
 

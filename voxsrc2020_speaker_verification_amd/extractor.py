@@ -124,6 +124,39 @@ class Extractor:
         check(lib().vox_plan_describe(self._h, C.c_void_p(x.data_ptr()), n, t, f, buf, need))
         return buf.value.decode().strip().split("\n")
 
+    # -- layer-by-layer parity support (tests) ------------------------------
+    def layer_outputs(self, x):
+        """Run the plan for the device batch x ([N,T,F] float32 torch tensor)
+        launch by launch and return (taps, embeddings): taps[i] is the output
+        of oracle layer i (oracle/models_ref.py `layers`) as a float32 numpy
+        array [n,h,w,c], read right after the launch that completes it."""
+        import torch
+        n, t, f = x.shape
+        out = torch.empty((n, self.dim), dtype=torch.float32, device=x.device)
+        L = lib()
+        xp, op = C.c_void_p(x.data_ptr()), C.c_void_p(out.data_ptr())
+        nops = C.c_int()
+        nt = check(L.vox_debug_taps(self._h, xp, n, t, f, op, None, 0, C.byref(nops)))
+        taps = (_native.Tap * max(nt, 1))()
+        check(L.vox_debug_taps(self._h, xp, n, t, f, op, taps, nt, C.byref(nops)))
+        torch.cuda.synchronize(x.device)
+        res, begin = [], 0
+        for tp in taps[:nt]:
+            check(L.vox_debug_run_ops(self._h, begin, tp.op_end, None))
+            begin = tp.op_end
+            es = 2 if tp.dtype == _native.VOX_BF16 else 4
+            rows = tp.n * tp.h * tp.w
+            raw = np.empty((rows, tp.ld * es), np.uint8)
+            check(L.vox_debug_read(raw.ctypes.data_as(C.c_void_p), C.c_void_p(tp.data), raw.nbytes))
+            if es == 2:
+                a = (raw.view(np.uint16)[:, :tp.c].astype(np.uint32) << 16).view(np.float32)
+            else:
+                a = raw.view(np.float32)[:, :tp.c].copy()
+            res.append(a.reshape(tp.n, tp.h, tp.w, tp.c))
+        # the rest of the plan: pooling + head
+        check(L.vox_debug_run_ops(self._h, begin, nops.value, None))
+        return res, out.cpu().numpy()
+
     # -- tf_extract chunk loop ---------------------------------------------
     def embed_utterance(self, feat):
         feat = np.ascontiguousarray(feat, dtype=np.float32)

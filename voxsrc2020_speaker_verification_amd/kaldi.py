@@ -159,11 +159,17 @@ def format_mat_flt(key, m):
 class VectorWriter:
     """`ark,scp:<base>.ark,<base>.scp` writer of float vectors (copy-vector)."""
 
-    def __init__(self, base):
+    def __init__(self, base, atomic=False):
+        """atomic=True: write <base>.ark/.scp under temporary names and rename
+        them into place on close (ark first, then scp), so an interrupted
+        writer never leaves a complete-looking pair (dp_extract --resume)."""
         self.ark_path = base + ".ark"
         self.scp_path = base + ".scp"
-        self._ark = open(self.ark_path, "wb")
-        self._scp = open(self.scp_path, "w")
+        self._atomic = atomic
+        sfx = f".part{os.getpid()}" if atomic else ""
+        self._ark = open(self.ark_path + sfx, "wb")
+        self._scp = open(self.scp_path + sfx, "w")
+        self._sfx = sfx
 
     def write(self, key, v):
         rec, off = format_vec_flt(key, v)
@@ -176,6 +182,9 @@ class VectorWriter:
             self._ark.close()
             self._scp.close()
             self._ark = self._scp = None
+            if self._atomic:
+                os.replace(self.ark_path + self._sfx, self.ark_path)
+                os.replace(self.scp_path + self._sfx, self.scp_path)
 
     def __enter__(self):
         return self
