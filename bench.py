@@ -110,29 +110,47 @@ def weights_blob(model, feat_dim, cache_dir):
     return data
 
 
-def cpu_baseline(model, feat_dim, T, blob, budget_s=12.0):
-    """The numpy fp32 oracle (kind "port") on a bounded sample."""
-    from oracle import models_ref
-    from voxsrc2020_speaker_verification_amd import synth, weights
-    spec, t = weights.load_blob(blob)
+def _host_info():
+    model = None
     try:
-        from threadpoolctl import threadpool_info
-        cores = max([i.get("num_threads", 1) for i in threadpool_info()
-                     if i.get("user_api") == "blas"] or [1])
-    except Exception:
-        cores = os.cpu_count() or 1
-    bs = 4
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return model, os.cpu_count() or 1
+
+
+def cpu_baseline(model, feat_dim, T, blob, budget_s=15.0):
+    """The C++/OpenMP fp32 restatement of the reference forward
+    (oracle/cpu/voxcpu.cpp, the stand-in for tf_extract.py's TF1 CPU
+    `sess.run`; kind "port") on a bounded sample of the same workload, on the
+    host cores this job may use: OMP_NUM_THREADS when set (16 on the GPU boxes,
+    a one-GPU job's CPU share), else every core."""
+    from oracle.cpu import CpuModel, build as cpu_build
+    from voxsrc2020_speaker_verification_amd import synth
+    cpu_build.build()
+    m = CpuModel(blob)
+    name, nproc = _host_info()
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or nproc
+    bs = 2 * threads
     x = synth.make_features(bs, T, feat_dim, seed=99)
+    m.run(x[:2], threads)                       # workspace + weights warm
     n, t0 = 0, time.perf_counter()
     while True:
-        models_ref.forward(spec, t, x)
+        m.run(x, threads)
         n += bs
         if time.perf_counter() - t0 >= budget_s:
             break
     el = time.perf_counter() - t0
-    return {"value": n / el, "unit": "utterances/sec", "cores": int(cores), "kind": "port",
-            "sample": f"{n} utterances of {T}x{feat_dim} in batches of {bs} "
-                      f"({el:.1f} s, numpy fp32 oracle, BLAS threads={cores})"}
+    avx512 = "avx512f" in open("/proc/cpuinfo").read() if os.path.exists("/proc/cpuinfo") else None
+    return {"value": round(n / el, 3), "unit": "utterances/sec", "cores": threads, "kind": "port",
+            "impl": "cpp_omp", "nproc": nproc, "cpu_model": name,
+            "isa": "avx512" if avx512 else "avx2",
+            "sample": f"{n} utterances of {T}x{feat_dim} in batches of {bs} ({el:.1f} s; "
+                      f"oracle/cpu/voxcpu.cpp fp32 C++/OpenMP, {threads} threads)"}
 
 
 def main():

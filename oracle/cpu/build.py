@@ -9,7 +9,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(HERE, "voxcpu.cpp")
 LIB = os.path.join(HERE, "libvoxcpu.so")
 # x86-64-v3 = AVX2 + FMA: every x86 host a GPU box here has (no AVX-512 assumed)
-FLAGS = ["-O3", "-march=x86-64-v3", "-fopenmp", "-std=c++17", "-shared", "-fPIC"]
+FLAGS = ["-O3", "-march=x86-64-v3", "--param=sra-max-scalarization-size-Ospeed=8192", "-fopenmp", "-std=c++17", "-shared", "-fPIC"]
 
 
 def build(force=False):

@@ -15,10 +15,14 @@
 //
 // Convolutions are NHWC implicit GEMMs: out[p][co] = sum_{tap,ci} x[pix(p,tap)][ci]
 // * w[tap][ci][co], with the HWIO weights re-packed per (group, 16-wide cout
-// block) as [K][16], and a 6-pixel x 16-cout register tile of 8-wide fp32
-// vectors (AVX2 FMA, -march=x86-64-v3) per inner step; OpenMP over (pixel
-// block, cout block).  BN is applied as (x - mean) * (1 / sqrt(var + eps)),
-// TF's formula, everything in float32.
+// block) as [K][16]; register tiles of 12 pixels x 32 couts (AVX-512, picked
+// at run time when the host has it) or 6 x 16 (AVX2 + FMA, the -march=x86-64-v3
+// baseline); OpenMP over (pixel block, cout block); BN / ReLU / residual /
+// the next split's addend fused into the conv epilogue.  BN is applied as
+// (x - mean) * (1 / sqrt(var + eps)), TF's formula, everything in float32.
+// Measured in this build container (8 Sapphire Rapids cores): res2net50 80x200
+// 15.7 utt/s = 350 GFLOP/s (AVX-512), 9.3 utt/s (AVX2); the numpy oracle ~6.6.
+#include <immintrin.h>
 #include <omp.h>
 
 #include <cmath>
@@ -33,8 +37,6 @@
 #include <vector>
 
 namespace {
-
-typedef float v8 __attribute__((vector_size(32)));
 
 thread_local std::string g_err;
 int fail(const std::string& m) {
@@ -130,47 +132,85 @@ struct Epi {
   int ldz = 0;
 };
 
-typedef float v16 __attribute__((vector_size(64)));
-
-// One (pixel block, 16-cout block(s)) unit of the implicit GEMM: MR pixels x
-// NB blocks of 16 couts, VW-float vectors; xr[t][i] = pixel i's input row at
-// tap t (or a zero row).
-template <int MR, int NB, typename V>
-static inline __attribute__((always_inline)) void conv_unit(const float* const* xr, int taps, int cig, const float* W, size_t bstride,
-                             float (*out)[NB * 16]) {
-  constexpr int VW = sizeof(V) / 4;
-  constexpr int NV = 16 / VW;  // vectors per 16-block
-  V acc[MR][NB * NV];
-  for (int i = 0; i < MR; ++i)
-    for (int j = 0; j < NB * NV; ++j) acc[i][j] = V{};
+// AVX-512 tile: 12 pixels x 32 couts (two packed 16-blocks), accumulators as
+// named registers (an accumulator array was kept in memory by the compiler)
+#define VOX_R12(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11)
+__attribute__((target("avx512f,avx512vl,avx512dq,avx512bw"))) static void conv_unit_512_12x2(
+    const float* const* xr, int taps, int cig, const float* W, size_t bstride, float (*out)[32]) {
+#define DECL(i) __m512 a##i##0 = _mm512_setzero_ps(), a##i##1 = _mm512_setzero_ps();
+  VOX_R12(DECL)
+#undef DECL
   for (int t = 0; t < taps; ++t) {
     const float* Wt = W + (size_t)t * cig * 16;
-    const float* xp[MR];
-    for (int i = 0; i < MR; ++i) xp[i] = xr[t * MR + i];
+#define PTR(i) const float* x##i = xr[t * 12 + i];
+    VOX_R12(PTR)
+#undef PTR
     for (int ci = 0; ci < cig; ++ci) {
-      V w[NB * NV];
-      for (int b = 0; b < NB; ++b)
-        for (int v = 0; v < NV; ++v) {
-          V t;
-          __builtin_memcpy(&t, Wt + b * bstride + ci * 16 + v * VW, sizeof(V));
-          w[b * NV + v] = t;
-        }
-#pragma GCC unroll 12
-      for (int i = 0; i < MR; ++i) {
-        const float a = xp[i][ci];
-        for (int j = 0; j < NB * NV; ++j) acc[i][j] += a * w[j];
-      }
+      const __m512 w0 = _mm512_loadu_ps(Wt + ci * 16), w1 = _mm512_loadu_ps(Wt + bstride + ci * 16);
+#define FMA(i)                                        \
+  {                                                   \
+    const __m512 b = _mm512_set1_ps(x##i[ci]);        \
+    a##i##0 = _mm512_fmadd_ps(b, w0, a##i##0);        \
+    a##i##1 = _mm512_fmadd_ps(b, w1, a##i##1);        \
+  }
+      VOX_R12(FMA)
+#undef FMA
     }
   }
-  for (int i = 0; i < MR; ++i)
-    for (int j = 0; j < NB * NV; ++j)
-      for (int e = 0; e < VW; ++e) out[i][j * VW + e] = acc[i][j][e];
+#define ST(i) _mm512_storeu_ps(out[i], a##i##0); _mm512_storeu_ps(out[i] + 16, a##i##1);
+  VOX_R12(ST)
+#undef ST
 }
 
-template <int MR, int NB>
-__attribute__((target("avx512f,avx512vl,avx512dq,avx512bw"))) static void conv_unit_512(
-    const float* const* xr, int taps, int cig, const float* W, size_t bstride, float (*out)[NB * 16]) {
-  conv_unit<MR, NB, v16>(xr, taps, cig, W, bstride, out);
+__attribute__((target("avx512f,avx512vl,avx512dq,avx512bw"))) static void conv_unit_512_12x1(
+    const float* const* xr, int taps, int cig, const float* W, size_t, float (*out)[32]) {
+#define DECL(i) __m512 a##i##0 = _mm512_setzero_ps();
+  VOX_R12(DECL)
+#undef DECL
+  for (int t = 0; t < taps; ++t) {
+    const float* Wt = W + (size_t)t * cig * 16;
+#define PTR(i) const float* x##i = xr[t * 12 + i];
+    VOX_R12(PTR)
+#undef PTR
+    for (int ci = 0; ci < cig; ++ci) {
+      const __m512 w0 = _mm512_loadu_ps(Wt + ci * 16);
+#define FMA(i) a##i##0 = _mm512_fmadd_ps(_mm512_set1_ps(x##i[ci]), w0, a##i##0);
+      VOX_R12(FMA)
+#undef FMA
+    }
+  }
+#define ST(i) _mm512_storeu_ps(out[i], a##i##0);
+  VOX_R12(ST)
+#undef ST
+}
+
+// AVX2 tile: 6 pixels x 16 couts (two 8-wide vectors), named accumulators
+#define VOX_R6(X) X(0) X(1) X(2) X(3) X(4) X(5)
+static void conv_unit_256_6x1(const float* const* xr, int taps, int cig, const float* W,
+                              float (*out)[16]) {
+#define DECL(i) __m256 a##i##0 = _mm256_setzero_ps(), a##i##1 = _mm256_setzero_ps();
+  VOX_R6(DECL)
+#undef DECL
+  for (int t = 0; t < taps; ++t) {
+    const float* Wt = W + (size_t)t * cig * 16;
+#define PTR(i) const float* x##i = xr[t * 6 + i];
+    VOX_R6(PTR)
+#undef PTR
+    for (int ci = 0; ci < cig; ++ci) {
+      const __m256 w0 = _mm256_loadu_ps(Wt + ci * 16), w1 = _mm256_loadu_ps(Wt + ci * 16 + 8);
+#define FMA(i)                                        \
+  {                                                   \
+    const __m256 b = _mm256_broadcast_ss(x##i + ci);  \
+    a##i##0 = _mm256_fmadd_ps(b, w0, a##i##0);        \
+    a##i##1 = _mm256_fmadd_ps(b, w1, a##i##1);        \
+  }
+      VOX_R6(FMA)
+#undef FMA
+    }
+  }
+#define ST(i) _mm256_storeu_ps(out[i], a##i##0); _mm256_storeu_ps(out[i] + 8, a##i##1);
+  VOX_R6(ST)
+#undef ST
 }
 
 // VOXCPU_NO_AVX512=1 forces the AVX2 kernel (A/B)
@@ -248,13 +288,13 @@ void conv2d(const Conv& c, const Act& x, int sh, int dh, int dw, int pt, int pl,
     float o[12][32];
     if (wide) {
       if (nbh == 2)
-        conv_unit_512<12, 2>(X, taps, c.cig, W, bstride, o);
+        conv_unit_512_12x2(X, taps, c.cig, W, bstride, o);
       else
-        conv_unit_512<12, 1>(X, taps, c.cig, W, bstride, reinterpret_cast<float(*)[16]>(&o[0][0]));
+        conv_unit_512_12x1(X, taps, c.cig, W, bstride, o);
     } else {
-      conv_unit<6, 1, v8>(X, taps, c.cig, W, bstride, reinterpret_cast<float(*)[16]>(&o[0][0]));
+      conv_unit_256_6x1(X, taps, c.cig, W, reinterpret_cast<float(*)[16]>(&o[0][0]));
     }
-    const int rowlen = (wide && nbh == 1) ? 16 : NBU * 16;
+    const int rowlen = wide ? 32 : 16;
     const float* ob = &o[0][0];
     for (int i = 0; i < MR; ++i) {
       if (!pv[i]) continue;

@@ -75,6 +75,16 @@ def load(root):
             r["valu_per_mfma"] = m.get("SQ_INSTS_VALU", 0) / m["SQ_INSTS_MFMA"]
         if m.get("SQ_LDS_IDX_ACTIVE"):
             r["lds_conflict_frac"] = m.get("SQ_LDS_BANK_CONFLICT", 0) / m["SQ_LDS_IDX_ACTIVE"]
+        # MFMA utilisation (MI355X_MICROARCH.md "rocprofv3 PMC"): busy cycles
+        # summed over the 1024 SIMDs against the dispatch's cycles, GRBM_GUI_ACTIVE
+        # being the sum over the 8 XCDs (per-XCD cycles = GUI / 8)
+        if m.get("GRBM_GUI_ACTIVE") and "SQ_VALU_MFMA_BUSY_CYCLES" in m:
+            cyc = m["GRBM_GUI_ACTIVE"] / 8.0
+            r["mfma_busy_frac"] = m["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024.0 * cyc)
+            r["gui_cycles"] = cyc
+            if m.get("SQ_INSTS_MFMA"):
+                # 16x16x32 bf16: 16 cycles per MFMA per SIMD (cycle-constants table)
+                r["mfma_issue_frac"] = m["SQ_INSTS_MFMA"] * 16.0 / (1024.0 * cyc)
         if m.get("SQ_WAVE_CYCLES"):
             w = m["SQ_WAVE_CYCLES"]
             r["wait_frac"] = m.get("SQ_WAIT_ANY", 0) / w
@@ -94,20 +104,21 @@ def main():
     if a.json:
         with open(a.json, "w") as f:
             json.dump(s, f, indent=1, sort_keys=True)
-    rows = ["| kernel | disp | VGPR/AGPR | LDS B | VALU/MFMA | LDS confl | wait / stall / active | HBM read MB | HBM write MB |",
-            "|---|---|---|---|---|---|---|---|---|"]
+    rows = ["| kernel | disp | VGPR/AGPR | LDS B | VALU/MFMA | LDS confl | wait / stall / active | HBM read MB | HBM write MB | MFMA busy |",
+            "|---|---|---|---|---|---|---|---|---|---|"]
     key = lambda kv: -kv[1].get("hbm_bytes", 0) - kv[1]["mean"].get("SQ_INSTS_MFMA", 0)
     for k, r in sorted(s.items(), key=key):
         if k.startswith("__amd"):
             continue
         f = lambda x, fmt: (fmt % x) if x is not None else "-"
-        rows.append("| %s | %d | %d/%d | %d | %s | %s | %s | %s | %s |" % (
+        rows.append("| %s | %d | %d/%d | %d | %s | %s | %s | %s | %s | %s |" % (
             k, r["mean"]["dispatches"], r["vgpr"], r["agpr"], r["lds"],
             f(r.get("valu_per_mfma"), "%.1f"), f(r.get("lds_conflict_frac"), "%.2f"),
             ("%.2f / %.2f / %.2f" % (r["wait_frac"], r["issue_stall_frac"], r["active_frac"]))
             if "wait_frac" in r else "-",
             f(r.get("hbm_read_bytes", None) and r["hbm_read_bytes"] / 1e6, "%.1f"),
-            f(r.get("hbm_write_bytes", None) and r["hbm_write_bytes"] / 1e6, "%.1f")))
+            f(r.get("hbm_write_bytes", None) and r["hbm_write_bytes"] / 1e6, "%.1f"),
+            f(r.get("mfma_busy_frac"), "%.3f")))
     txt = "\n".join(rows)
     if a.md:
         with open(a.md, "w") as f:
