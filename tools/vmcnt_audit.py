@@ -191,6 +191,9 @@ def _cfg(ins):
     return bl, succs
 
 
+WRITES_ONLY = "--writes" in sys.argv
+
+
 def _step(insn, q, hits=None, bi=None):
     """Advance the in-flight queue q (list of dest-register tuples, oldest
     first; () for stores) over one instruction; record hits."""
@@ -217,6 +220,12 @@ def _step(insn, q, hits=None, bi=None):
             q.append(())
     else:
         bad = used & pend
+        if WRITES_ONLY:
+            # the first operand of a VALU / DS read is its destination
+            ops = insn[len(op):].split(",")
+            dst = regs(ops[0]) if (op.startswith("v_") and not op.startswith("v_cmp")) or \
+                op.startswith("ds_read") else set()
+            bad = dst & pend
     if bad and hits is not None:
         hits.append((bi, insn, sorted(bad)))
 

@@ -196,8 +196,8 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
   }
 
   // ---- input rows: global -> registers (prefetch) -> LDS
-  // two register sets each for the input rows and the residual rows: a row is
-  // requested two steps before it is used (HBM latency under load exceeds a step)
+  // two register sets for the input rows: a row is requested two steps before
+  // it is used (HBM latency under load exceeds a step)
   vu32x4 inr[2][K::IREG];
   const int nres = is_c ? PT : 0;                               // residual loads per step
   const int nst = ((q.dbg & 256) && blockIdx.x == 0) ? 1 : 0;  // trace stamps (stores)
@@ -208,7 +208,7 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
   // Each load is always issued (rows outside the image read a zero line), so
   // the per-step op counts are wave-uniform:
   //   phase 0: 1x1c waves: ns stores (PT when row c is owned, else 0) then PT
-  //            residual loads (row c+2); phase 1: IREG input loads (row a+3).
+  //            residual loads (row c+1); phase 1: IREG input loads (row a+3).
   const bf16_t* zline = reinterpret_cast<const bf16_t*>(g_vox_zero);
   auto load_in = [&](auto P, int r) __attribute__((always_inline)) {
 #pragma unroll
@@ -228,8 +228,10 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
       if (c < 16 * PT * K::CU) *reinterpret_cast<vu32x4*>(inb + px * K::ISTR + u * 16) = inr[P][i];
     }
   };
-  vu32x4 resb[2][PT];
-  auto load_res = [&](auto P, int r) __attribute__((always_inline)) {
+  // the residual row is requested one step ahead (a second register set would
+  // push the chain's fragment reads onto the registers they are consumed from)
+  vu32x4 resb[PT];
+  auto load_res = [&](int r) __attribute__((always_inline)) {
     if (!is_c) return;
 #pragma unroll
     for (int j = 0; j < PT; ++j) {
@@ -238,7 +240,7 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
       // the (CI = 32)-channel input row, for the shortcut MFMAs
       const int cho = K::PROJ ? 8 * g : 32 * pq + 8 * g;
       const bool ok = r >= h0 && r < h1 && px < W;
-      resb[P][j] = vld16(ok ? (const void*)(X + (img + (size_t)r * W + px) * CI + cho) : zline);
+      resb[j] = vld16(ok ? (const void*)(X + (img + (size_t)r * W + px) * CI + cho) : zline);
     }
   };
 
@@ -260,13 +262,12 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
   store_in(P0{});
   load_in(P0{}, a0 + 1);
   load_in(P1{}, a0 + 2);
-  load_res(P0{}, a0 - K::LAG_C);
-  load_res(P1{}, a0 - K::LAG_C + 1);
+  load_res(a0 - K::LAG_C);
   __syncthreads();
   int ns_prev = 0;   // stores this wave issued in the previous step
 
-  // step t (register set P = t & 1): rows a + 1 (input) and c (residual) were
-  // requested two steps earlier
+  // step t (register set P = t & 1): input row a + 1 was requested two steps
+  // earlier, residual row c one step earlier
   const bool trace = (q.dbg & 256) && blockIdx.x == 0 && lane == 0;
   auto stamp = [&](int t, int i) __attribute__((always_inline)) {
     if (trace && t < 512) g_vox_trace[(wave * 512 + t) * 4 + i] = __builtin_amdgcn_s_memtime();
@@ -274,7 +275,7 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
   auto step = [&](auto P, int t) __attribute__((always_inline)) {
     const int a = a0 + t;
     const int c = a - K::LAG_C;
-    auto& res = resb[P];
+    auto& res = resb;
     const bool cstep = is_c && c >= h0 && c < h1 && !(q.dbg & 2);
     const int ns_cur = cstep ? PT : 0;
     stamp(t, 0);
@@ -328,9 +329,9 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
         if (two) epi(c0, c1, px + 16);
       }
     } else if (cstep) {
-      // residual row c (loaded at step t-2): younger are that step's trace
-      // stamps and input loads, step t-1's stores, residual and input loads
-      vm_wait(t < 2 ? 0 : 2 * K::IREG + PT + ns_prev + 7 * nst);
+      // residual row c (loaded at step t-1, after its stores): younger are
+      // that step's input loads and 3 trace stamps, and this step's first stamp
+      vm_wait(t < 1 ? 0 : K::IREG + 4 * nst);
 #pragma unroll
       for (int j = 0; j < PT; ++j) vm_launder(res[j]);
       // B chunk s of lane group g: concat channel 32s+8g -> (plane, offset)
@@ -404,17 +405,17 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
         if (two) epi(c0, c1, __builtin_bit_cast(bf16x8, res[(j + 1) < PT ? j + 1 : j]), px + 16);
       }
     } else if (is_c) {
-      // row c is outside the segment: the residual set requested two steps ago
-      // is not consumed, but load_res below reuses its registers.  Retire it
-      // first on this path too -- otherwise those registers are dead to the
-      // compiler while the loads are in flight, it builds the next addresses in
-      // them, and the late data (the zero line at the segment start) lands on
-      // an address: the illegal-address fault of the one-step variant (9c1d9bf)
-      vm_wait(t < 2 ? 0 : 2 * K::IREG + PT + ns_prev + 7 * nst);
+      // row c is outside the segment: the residual row requested at step t-1 is
+      // not consumed, but load_res below reuses its registers.  Retire it first
+      // on this path too -- otherwise those registers are dead to the compiler
+      // while the loads are in flight, it builds the next addresses in them, and
+      // the late data (the zero line at the segment start) lands on an address:
+      // the intermittent illegal-address fault of 9c1d9bf (DESIGN.md "vmcnt")
+      vm_wait(t < 1 ? 0 : K::IREG + 4 * nst);
 #pragma unroll
       for (int j = 0; j < PT; ++j) vm_launder(res[j]);
     }
-    if (!(q.dbg & 8)) load_res(P, c + 2);
+    if (!(q.dbg & 8)) load_res(c + 1);
     stamp(t, 1);
     __syncthreads();
     stamp(t, 2);
@@ -473,26 +474,28 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
         }
       };
       // the PT pixel tiles as independent accumulators, fragments read one
-      // k-step ahead (same K order per tile)
+      // k-step ahead into the other of two register sets (same K order per
+      // tile); a single set rotated by copies let the compiler merge the two
+      // and issue each read only after the MFMA that freed its register
       f32x4 acc[PT];
-      bf16x8 bc[PT], bn[PT];
+      bf16x8 fr[2][PT];
 #pragma unroll
       for (int j = 0; j < PT; ++j) {
         acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-        bc[j] = *reinterpret_cast<const bf16x8*>(zring + boff[0] + 16 * j * ASTR);
+        fr[0][j] = *reinterpret_cast<const bf16x8*>(zring + boff[0] + 16 * j * ASTR);
       }
 #pragma unroll
       for (int s = 0; s < KST; ++s) {
         if (s + 1 < KST) {
 #pragma unroll
           for (int j = 0; j < PT; ++j)
-            bn[j] = *reinterpret_cast<const bf16x8*>(zring + boff[s + 1] + 16 * j * ASTR);
+            fr[(s + 1) & 1][j] = *reinterpret_cast<const bf16x8*>(zring + boff[s + 1] + 16 * j * ASTR);
+          __builtin_amdgcn_sched_group_barrier(0x100, PT, 0);   // the reads first
         }
 #pragma unroll
-        for (int j = 0; j < PT; ++j) acc[j] = mfma_step(wb[s], bc[j], acc[j]);
-#pragma unroll
-        for (int j = 0; j < PT; ++j) bc[j] = bn[j];
-        __builtin_amdgcn_sched_barrier(0);   // reads stay one k-step ahead
+        for (int j = 0; j < PT; ++j) acc[j] = mfma_step(wb[s], fr[s & 1][j], acc[j]);
+        if (s + 1 < KST) __builtin_amdgcn_sched_group_barrier(0x008, PT, 0);   // then the MFMAs
+        __builtin_amdgcn_sched_barrier(0);
       }
 #pragma unroll
       for (int j = 0; j < PT; ++j) epilogue(acc[j], 16 * j + col);
@@ -509,7 +512,7 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
 #pragma unroll
   for (int i = 0; i < K::IREG; ++i) { vm_launder(inr[0][i]); vm_launder(inr[1][i]); }
 #pragma unroll
-  for (int j = 0; j < PT; ++j) { vm_launder(resb[0][j]); vm_launder(resb[1][j]); }
+  for (int j = 0; j < PT; ++j) vm_launder(resb[j]);
 }
 
 template <int CI, int C, int WID, int S, int PT>

@@ -50,6 +50,12 @@ __device__ __forceinline__ bf16x8 relu_bf16(bf16x8 v) {
 // waits for every store the wave has in flight.  A value loaded with vld16 is
 // valid only after vm_wait(n) (n = this wave's vector-memory ops issued after
 // it) and vm_launder(v) (so the compiler does not hoist uses above the wait).
+// Soundness rule: on EVERY path from a vld16 the wave must reach a covering
+// vm_wait followed by vm_launder of the destination before the variable is
+// reassigned or the kernel ends.  The compiler does not know the load is in
+// flight: where the value is dead on some path (never laundered there), it
+// reuses the registers at once -- e.g. for the next loads' addresses -- and the
+// late data then overwrites them (tools/vmcnt_audit.py checks the ISA).
 // No "memory" clobbers: the kernels never read back what these touch, and a
 // clobber would pin every LDS access around each store.
 typedef unsigned vu32x4 __attribute__((ext_vector_type(4)));

@@ -1379,10 +1379,94 @@ __global__ __launch_bounds__(64 * TS) void stats_pool_k(const T* __restrict__ x,
   }
 }
 
+// Short utterance axis (H <= HM, bf16): one thread per 8-channel column of
+// one (n, w), all H rows requested at once into registers (raw bf16, 4 VGPRs
+// a row), both passes of tf.nn.moments from those registers, no LDS and no
+// barrier: every byte is read once with H loads in flight per thread.
+// Sequential summation over h (a fixed order per column, batch-independent).
+template <int HM>
+__global__ __launch_bounds__(256) void stats_pool_col(const bf16_t* __restrict__ x, int N, int H,
+                                                      int W, int C,
+                                                      const float* __restrict__ mean,
+                                                      const float* __restrict__ inv,
+                                                      float* __restrict__ out) {
+  const int chunks = C / 8;
+  const int64_t gcol = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (gcol >= (int64_t)N * W * chunks) return;
+  const int n = (int)(gcol / ((int64_t)W * chunks));
+  const int r = (int)(gcol - (int64_t)n * W * chunks);
+  const int w = r / chunks, ch = r - (r / chunks) * chunks;
+  const bf16_t* base = x + ((size_t)n * H * W + w) * C + (size_t)ch * 8;
+  const size_t rowstride = (size_t)W * C;
+  bf16x8 v[HM];
+#pragma unroll
+  for (int h = 0; h < HM; ++h)
+    if (h < H) v[h] = ld16(base + (size_t)h * rowstride);
+  float s[8], q[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s[e] = q[e] = 0.f;
+#pragma unroll
+  for (int h = 0; h < HM; ++h)
+    if (h < H) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s[e] += (float)v[h][e];
+    }
+  float mu[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) mu[e] = s[e] / (float)H;
+  // the rows stay packed bf16 between the passes (4 VGPRs each): without this the
+  // compiler keeps every converted float of pass 1 live for pass 2 (256 VGPRs)
+#pragma unroll
+  for (int h = 0; h < HM; ++h) {
+    vu32x4 t = __builtin_bit_cast(vu32x4, v[h]);
+    asm volatile("" : "+v"(t));
+    v[h] = __builtin_bit_cast(bf16x8, t);
+  }
+#pragma unroll
+  for (int h = 0; h < HM; ++h)
+    if (h < H) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float d = (float)v[h][e] - mu[e];
+        q[e] += d * d;
+      }
+    }
+  float* o = out + (size_t)n * W * 2 * C + (size_t)w * 2 * C + (size_t)ch * 8;
+  f32x4 om[2], os[2];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    float sd = sqrtf(q[e] / (float)H + 1e-5f);
+    float m = mu[e];
+    const int fm = w * 2 * C + ch * 8 + e, fs = fm + C;
+    if (mean) {
+      m = (m - mean[fm]) * inv[fm];
+      sd = (sd - mean[fs]) * inv[fs];
+    }
+    om[e >> 2][e & 3] = m;
+    os[e >> 2][e & 3] = sd;
+  }
+  *reinterpret_cast<f32x4*>(o) = om[0];
+  *reinterpret_cast<f32x4*>(o + 4) = om[1];
+  *reinterpret_cast<f32x4*>(o + C) = os[0];
+  *reinterpret_cast<f32x4*>(o + C + 4) = os[1];
+}
+
 template <typename T, int VN>
 static hipError_t stats_pool_ts(const T* x, int N, int H, int W, int C, const float* mean,
                                 const float* inv, float* out, hipStream_t s) {
   const int64_t cols = (int64_t)N * W * (C / VN);
+  if constexpr (sizeof(T) == 2 && VN == 8) {
+    if (H <= 32) {
+      const unsigned b = (unsigned)((cols + 255) / 256);
+      if (H <= 16)
+        hipLaunchKernelGGL((stats_pool_col<16>), dim3(b), dim3(256), 0, s, x, N, H, W, C, mean, inv, out);
+      else if (H <= 25)   // T = 200 at layer 4 (the headline)
+        hipLaunchKernelGGL((stats_pool_col<25>), dim3(b), dim3(256), 0, s, x, N, H, W, C, mean, inv, out);
+      else
+        hipLaunchKernelGGL((stats_pool_col<32>), dim3(b), dim3(256), 0, s, x, N, H, W, C, mean, inv, out);
+      return hipGetLastError();
+    }
+  }
   const unsigned blocks = (unsigned)((cols + 63) / 64);
   // more time-slices when there are few columns or many frames
   if (H >= 64 && blocks < 2048) {
