@@ -506,3 +506,48 @@ def test_run_device_new_buffers_without_sync(weights):
         ref = [ex.run(x) for x in xs]
     for g, r in zip(got, ref + [ref[0]]):
         assert np.array_equal(g, r)
+
+
+@pytest.mark.parametrize("name,F,T,N", [("dpn68", 80, 64, 2), ("dpn68", 40, 97, 3), ("dpn68", 80, 600, 2)])
+def test_gemm_ws_prologue_bitwise(weights, name, F, T, N, monkeypatch):
+    """DPN68's BN+ReLU-prologue 1x1 convs (>= 192 couts) on gemm1x1_ws<.., GS_PRO>:
+    prologue on the B fragments, K padded to 32 over finite neighbouring
+    channels, partial last cout tile, residual below ysplit + appended dense
+    channels -- the same bits as the gemm1x1_pipe / register-resident paths."""
+    import torch
+    from voxsrc2020_speaker_verification_amd import synth
+    spec, t, blob = weights(name, F)
+    x = synth.make_features(N, T, F, seed=19)
+    with _extractor(blob, "bf16") as ex:
+        got = ex.run(x)
+        pro = [l for l in ex.describe(torch.from_numpy(x).cuda())
+               if l.startswith("gemmwide") and "pro=1" in l]
+        assert len(pro) >= 5, len(pro)
+    monkeypatch.setenv("VOXEMB_NO_GEMM_WIDE", "1")
+    with _extractor(blob, "bf16") as ex:
+        ref = ex.run(x)
+    assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("F,T,N", [(80, 200, 64), (40, 320, 5), (40, 37, 3)])
+def test_gemm_ws_taps_bitwise(weights, F, T, N, monkeypatch):
+    """TDNN dilated convs (k5d1, k3d2, k3d3) on gemm1x1_ws<.., GS_TAPS>: every
+    tap's rows gathered by the loader waves, zero rows outside the utterance
+    (SAME), K = taps x cinp with a padded first layer -- the same bits as the
+    generic implicit GEMM, which sums the same tap-major 32-channel K steps
+    (the window-staged conv chunks K by channel blocks first at Cin 512)."""
+    import torch
+    from voxsrc2020_speaker_verification_amd import synth
+    spec, t, blob = weights("tdnn", F)
+    x = synth.make_features(N, T, F, seed=23)
+    with _extractor(blob, "bf16") as ex:
+        got = ex.run(x)
+        desc = ex.describe(torch.from_numpy(x).cuda())
+        assert sum(l.startswith("gemmwide") and "k=3x1" in l for l in desc) == 2, desc
+    monkeypatch.setenv("VOXEMB_NO_GEMM_TAPS", "1")
+    monkeypatch.setenv("VOXEMB_NO_WIN", "1")
+    with _extractor(blob, "bf16") as ex:
+        ref = ex.run(x)
+        assert not any(l.startswith("gemmwide") and "k=3x1" in l
+                       for l in ex.describe(torch.from_numpy(x).cuda()))
+    assert np.array_equal(got, ref)

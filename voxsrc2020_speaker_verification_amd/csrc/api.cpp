@@ -253,7 +253,8 @@ struct vox_model {
   bool no_conv3_utt = false;   // VOXEMB_NO_CONV3_UTT=1: conv3x3_pipe for the w = 192 stride-1 branches
   bool no_gconv = false;       // VOXEMB_NO_GCONV=1: grouped 3x3 on the generic implicit GEMM
   bool no_conv3 = false;
-  bool no_gemm_pro = false;    // VOXEMB_NO_GEMM_PRO=1: prologue 1x1 convs off the pipelined GEMM       // VOXEMB_NO_CONV3=1: Res2Net w>=96 3x3 branches on conv_win/igemm
+  bool no_gemm_pro = false;    // VOXEMB_NO_GEMM_PRO=1: prologue 1x1 convs off the LDS-DMA GEMMs
+  bool no_gemm_taps = false;   // VOXEMB_NO_GEMM_TAPS=1: TDNN dilated convs off gemm1x1_ws
   int num_cu = 256;            // compute units (persistent grids)
   int gemm_var = 0;            // VOXEMB_GEMM_VAR: gemm1x1_pipe variant (A/B experiments)
   int gemm_min_k = 128;        // VOXEMB_GEMM_MIN_K: smallest K routed to the LDS GEMMs (the K = 128
@@ -314,17 +315,23 @@ static int make_conv(vox_model* m, const HostTensor& k, int groups, const HostTe
   } else {
     HIPCHK(hipMemcpy(out.w->p, w.data(), w.size() * 4, hipMemcpyHostToDevice));
   }
-  if (dt == BF16 && groups == 1 && taps == 1 && out.vec && out.coutp % 32 == 0) {
+  // 1-D taps along H (TDNN kernels [k,1,Cin,Cout]): the same paired / blocked
+  // layouts with K = tap * cinp + ci, for gemm1x1_ws<.., GS_TAPS>
+  const bool taps1d = kw == 1 && kh > 1 && out.vec && out.cinp % 32 == 0;
+  if (dt == BF16 && groups == 1 && (taps == 1 || taps1d) && out.vec && out.coutp % 32 == 0) {
     // paired rows: row (2q+u)*16 + 4g + e <- channel 32q + 8g + 4u + e;
-    // rows padded with zeros to a multiple of 128 (gemm1x1_lds cout tiles)
-    const int rows = (out.coutp + 127) / 128 * 128;
+    // rows padded with zeros to a multiple of 256 (gemm1x1_lds 128-row and
+    // gemm1x1_ws 256-row cout tiles, incl. a partial last tile)
+    const int rows = (out.coutp + 255) / 256 * 256;
     std::vector<uint16_t> h((size_t)rows * out.kp, 0);
     for (int row = 0; row < out.coutp; ++row) {
       const int q = row / 32, u = (row / 16) & 1, g = (row & 15) / 4, e = row & 3;
       const int co = 32 * q + 8 * g + 4 * u + e;
       if (co >= cout) continue;
-      for (int ci = 0; ci < cin; ++ci)
-        h[(size_t)row * out.kp + ci] = f2bf(k.data[(size_t)ci * cout_all + col0 + co]);
+      for (int t = 0; t < taps; ++t)
+        for (int ci = 0; ci < cin; ++ci)
+          h[(size_t)row * out.kp + (size_t)t * out.cinp + ci] =
+              f2bf(k.data[((size_t)t * cin + ci) * cout_all + col0 + co]);
     }
     out.wpair = std::make_shared<DevBuf>();
     HIPCHK(out.wpair->ensure(h.size() * 2));
@@ -652,9 +659,40 @@ static void emit_conv(Builder& B, const ConvW& cw, Act x, const void* x2, int ld
       }
     }
   }
+  // bf16 1x1 with a BN+ReLU input prologue (DPN bn_relu_conv, >= 192 couts):
+  // the wave-specialised GEMM applies it to its B fragments
+  // (gemm1x1_ws<.., GS_PRO>; a padded K reads finite neighbouring channels
+  // that the prologue zeroes, slots carry slack for the last row)
+  if (op.type != 18 && op.type != 21 && B.m->dt == BF16 && dt_override != F32 && in_mean &&
+      cw.wblk && !B.m->no_gemm_wide && !B.m->no_gemm_pro && !(flags & EPI_PARTIAL) && ph == 0 &&
+      pw == 0 && cw.kh == 1 && cw.kw == 1 && cw.groups == 1 && cw.cout >= 192 && cw.cout % 8 == 0 &&
+      ldy % 8 == 0 && (ysplit >= (1 << 30) || (ysplit % 8 == 0 && ldy2 % 8 == 0)) &&
+      (!res || ldr % 8 == 0) && x.ld % 8 == 0) {
+    ConvParams q = p;
+    q.w = cw.wpair->p;
+    q.wblk = cw.wblk->p;
+    if (gemm_wide_bn(q)) {
+      p = q;
+      op.type = 21;
+    }
+  }
+  // 1-D dilated taps along time (TDNN, W = 1): the wave-specialised GEMM
+  // gathers every tap's input rows itself (gemm1x1_ws<.., GS_TAPS>)
+  if (op.type == 0 && B.m->dt == BF16 && dt_override != F32 && cw.wblk && cw.groups == 1 &&
+      cw.kw == 1 && cw.kh > 1 && x.W == 1 && Wo == 1 && Ho == x.H && sh == 1 && sw == 1 &&
+      pw == 0 && !in_mean && !x2 && !res && !(flags & EPI_PARTIAL) && !B.m->no_gemm_wide &&
+      !B.m->no_gemm_taps && x.ld % 8 == 0 && ldy % 8 == 0 && ysplit >= (1 << 30)) {
+    ConvParams q = p;
+    q.w = cw.wpair->p;
+    q.wblk = cw.wblk->p;
+    if (gemm_wide_bn(q)) {
+      p = q;
+      op.type = 21;
+    }
+  }
   // bf16 1x1 with a BN+ReLU input prologue (DPN bn_relu_conv): the pipelined
   // GEMM applies the prologue to its pixel fragments (gemm1x1_pipe<.., PRO>)
-  if (op.type != 18 && B.m->dt == BF16 && dt_override != F32 && in_mean && cw.wpair &&
+  if (op.type != 18 && op.type != 21 && B.m->dt == BF16 && dt_override != F32 && in_mean && cw.wpair &&
       !B.m->no_gemm_pipe && !B.m->no_gemm_pro && !(flags & EPI_PARTIAL) && ph == 0 && pw == 0 &&
       cw.kh == 1 && cw.kw == 1 && cw.groups == 1 && cw.cout % 8 == 0 && ldy % 8 == 0 &&
       (ysplit >= (1 << 30) || (ysplit % 8 == 0 && ldy2 % 8 == 0)) && (!res || ldr % 8 == 0) &&
@@ -1414,7 +1452,9 @@ static int build_plan(vox_model* m, const float* x, int n, int t, float* out) {
   }
   int rc = run(true);
   if (rc) return rc;
-  for (int s = 0; s < S_NSLOTS; ++s) HIPCHK(m->slots[s].ensure(m->slot_need[s]));
+  // slack: kernels with a K padded to 32 (gemm1x1_ws prologue / taps) read up to
+  // 62 B past the last row of their input
+  for (int s = 0; s < S_NSLOTS; ++s) HIPCHK(m->slots[s].ensure(m->slot_need[s] + 4096));
   rc = run(false);
   if (rc) return rc;
   m->plan_n = n;
@@ -1520,6 +1560,7 @@ extern "C" int vox_load_blob(const void* blob, size_t nbytes, int device, int pr
   if (const char* e = std::getenv("VOXEMB_NO_GCONV")) m->no_gconv = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_NO_CONV3")) m->no_conv3 = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_NO_GEMM_PRO")) m->no_gemm_pro = std::atoi(e) != 0;
+  if (const char* e = std::getenv("VOXEMB_NO_GEMM_TAPS")) m->no_gemm_taps = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_GEMM_VAR")) m->gemm_var = std::atoi(e);
   if (const char* e = std::getenv("VOXEMB_GEMM_MIN_K")) m->gemm_min_k = std::atoi(e);
   if (const char* e = std::getenv("VOXEMB_NO_CHAIN")) m->no_chain = std::atoi(e) != 0;

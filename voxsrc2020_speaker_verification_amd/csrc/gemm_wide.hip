@@ -86,6 +86,7 @@ __device__ __forceinline__ int gw_swz(int r) { return (4 - ((r >> 2) & 3)) & 3; 
 }  // namespace
 
 __device__ uint4 g_gw_sink[64];   // destination of masked lanes' stores
+__device__ uint4 g_gw_zero[4] = {};   // source of the B rows outside an utterance (1-D taps)
 
 #pragma clang fp contract(off)
 // DBG (diagnostics only, VOXEMB_GEMM_VAR): 1 = no MFMA / fragment reads,
@@ -361,8 +362,19 @@ constexpr int GS_NL = 4;   // loader waves
 // then hold 96 accumulators and fit the cap; the residual takes 3 phases)
 // DBG (diagnostics, VOXEMB_GEMM_VAR 21/22): 1 = compute waves skip fragment
 // reads and MFMAs (stores kept), 2 = loaders issue no DMA; results garbage
-template <int BN, bool RES, int BM = GW_BM, int DBG = 0>
+// MODE (operand variants; 0 = the Res2Net 1x1s):
+//   GS_PRO : BN + ReLU prologue on the B fragments, relu((x - m[k]) * inv[k])
+//            rounded to bf16, as gemm1x1_pipe<.., PRO> (DPN bn_relu_conv,
+//            dpn_model.py:40-45); channels k >= Cin of a padded K get m = inv = 0
+//   GS_TAPS: 1-D dilated conv along H (W = 1, the TDNN layers,
+//            tdnn_model.py:24-30): K = taps x cinp, k-step -> (tap, channel
+//            chunk), B row of pixel (n, h) at tap t = input row h + t dh - ph of
+//            the same utterance, a zero row outside it (SAME padding)
+constexpr int GS_PRO = 1, GS_TAPS = 2;
+template <int BN, bool RES, int BM = GW_BM, int DBG = 0, int MODE = 0>
 __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
+  constexpr bool PRO = (MODE & GS_PRO) != 0, TAPS = (MODE & GS_TAPS) != 0;
+  static_assert(!(PRO && TAPS), "one operand variant");
   constexpr int NI = BN / 32;
   constexpr int NQ = NI / 2;
   constexpr int NJ = BM / 64;                // 16-pixel columns per wave
@@ -420,6 +432,15 @@ __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
       tab[p.coutp + k] = k < p.Cout ? p.inv[k] : 0.f;
     }
   }
+  // prologue table [kp] means, [kp] inverses (zero past Cin: padded K reads
+  // finite neighbouring channels, relu((x - 0) * 0) = 0)
+  float* ptab = tab + 2 * p.coutp;
+  if constexpr (PRO) {
+    for (int k = tid; k < p.kp; k += GS_NT) {
+      ptab[k] = k < p.Cin ? p.in_mean[k] : 0.f;
+      ptab[p.kp + k] = k < p.Cin ? p.in_inv[k] : 0.f;
+    }
+  }
   __syncthreads();
 
   if (loader) {
@@ -431,6 +452,8 @@ __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
     const bool blk = Wb != nullptr && !(DBG & 4);
     const int wstep = blk ? 512 : 32;   // elements per k-step of a weight piece
     int l_tile = 0, l_k = 0, l_co0 = 0, l_px0 = 0;
+    int tho[NLL];   // GS_TAPS: the B row's time index (its utterance base is in src)
+    const bf16_t* zero = reinterpret_cast<const bf16_t*>(g_gw_zero);
     auto set_load_tile = [&](int tj) {
       const int lid = t_first + tj * t_step;
       l_co0 = (lid % cblocks) * BN;
@@ -449,7 +472,12 @@ __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
           const int pix = min(l_px0 + row - BN, M - 1);
           const int n = pix / HoWo, rr = pix - n * HoWo;
           const int ho = rr / p.Wo, wo = rr - ho * p.Wo;
-          src[i] = X + (((size_t)n * p.H + ho * p.sh) * p.W + wo * p.sw) * p.ldx + c * 8;
+          if constexpr (TAPS) {
+            src[i] = X + (size_t)n * p.H * p.ldx + c * 8;   // W = 1: row h at h * ldx
+            tho[i] = ho;
+          } else {
+            src[i] = X + (((size_t)n * p.H + ho * p.sh) * p.W + wo * p.sw) * p.ldx + c * 8;
+          }
         }
       }
     };
@@ -457,11 +485,20 @@ __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
     auto issue = [&](int slot) -> int {
       int n = 0;
       if (l_k < KT) {
+        // GS_TAPS: this k-step's tap and channel chunk (wave-uniform)
+        const int tap = TAPS ? (32 * l_k) / p.cinp : 0;
+        const int ci0 = TAPS ? 32 * l_k - tap * p.cinp : 0;
+        const int sh_t = TAPS ? tap * p.dh - p.ph : 0;
 #pragma unroll
         for (int i = 0; i < NLL; ++i) {
           const int gi = lw + GS_NL * i;
           const int kst = i < BN / 64 ? wstep : 32;   // gi < BN/16 <=> i < BN/64
-          if (!(DBG & 2)) gw_glds16(src[i] + l_k * kst, lds0 + (uint32_t)slot * GW_SLOT + (uint32_t)gi * 1024u);
+          const bf16_t* a = src[i] + l_k * kst;
+          if (TAPS && i >= BN / 64) {
+            const int hi = tho[i] + sh_t;
+            a = (hi >= 0 && hi < p.H) ? src[i] + (size_t)hi * p.ldx + ci0 : zero;
+          }
+          if (!(DBG & 2)) gw_glds16(a, lds0 + (uint32_t)slot * GW_SLOT + (uint32_t)gi * 1024u);
         }
         n = (DBG & 2) ? 0 : NLL;
       } else if (RES) {
@@ -588,6 +625,22 @@ __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
       bf16x8 a[NI], b[NJ];
 #pragma unroll
       for (int j = 0; j < NJ; ++j) b[j] = *reinterpret_cast<const bf16x8*>(L + offb + j * 1024);
+      if constexpr (PRO) {
+        // this lane's 8 K channels of the step: prologue on every B fragment
+        const int kb = 32 * c_k + 8 * g;
+        const f32x4 m0 = *reinterpret_cast<const f32x4*>(ptab + kb);
+        const f32x4 m1 = *reinterpret_cast<const f32x4*>(ptab + kb + 4);
+        const f32x4 i0 = *reinterpret_cast<const f32x4*>(ptab + p.kp + kb);
+        const f32x4 i1 = *reinterpret_cast<const f32x4*>(ptab + p.kp + kb + 4);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            b[j][e] = (bf16_t)fmaxf(((float)b[j][e] - m0[e]) * i0[e], 0.f);
+            b[j][4 + e] = (bf16_t)fmaxf(((float)b[j][4 + e] - m1[e]) * i1[e], 0.f);
+          }
+        }
+      }
       a[0] = *reinterpret_cast<const bf16x8*>(L + offa);
       a[1] = *reinterpret_cast<const bf16x8*>(L + offa + 1024);
 #pragma unroll
@@ -625,11 +678,17 @@ __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
 
 // BN of the wide tile for this conv, or 0 if gemm1x1_wide does not apply
 int gemm_wide_bn(const ConvParams& p) {
-  if (p.in_mean || p.kp % 32 || p.kp / 32 < 3 || p.Cout % 8) return 0;
+  if (p.kp % 32 || p.kp / 32 < 3 || p.Cout % 8) return 0;
+  if (p.in_mean && (!p.in_inv || (p.kh != 1 || p.kw != 1))) return 0;
+  if (p.kh > 1 && (p.in_mean || p.kw != 1 || p.W != 1 || p.Wo != 1 || p.sh != 1 || p.cinp % 32 ||
+                   p.kp != p.kh * p.cinp || p.Ho != p.H))
+    return 0;
   const int M = p.N * p.Ho * p.Wo;
   int bn = 0;
   if (p.Cout % 256 == 0) bn = 256;
   else if (p.Cout % 192 == 0 && !(p.flags & EPI_RES)) bn = 192;
+  // DPN prologue convs: partial last cout tile (the weights hold 256-row multiples)
+  else if (p.in_mean && p.Cout >= 192) bn = 256;
   if (!bn || p.Cout > 2048) return 0;
   if ((p.flags & EPI_RES) && (!p.res || p.ldr % 8)) return 0;
   const int T = ((M + GW_BM - 1) / GW_BM) * (p.Cout / bn);
@@ -650,12 +709,36 @@ hipError_t launch_gemm_wide(const ConvParams& p0, int num_cu, int variant, hipSt
   const int bn = gemm_wide_bn(p0);
   if (!bn) return hipErrorInvalidValue;
   ConvParams p = p0;
-  p.coutp = p.Cout;   // whole BN blocks (the weights hold >= roundup128(Cout) rows)
+  // whole BN blocks (the weights hold roundup256(Cout) rows; extra couts are masked)
+  p.coutp = (p.Cout + bn - 1) / bn * bn;
   const int M = p.N * p.Ho * p.Wo;
-  const int T = ((M + GW_BM - 1) / GW_BM) * (p.Cout / bn);
+  const int T = ((M + GW_BM - 1) / GW_BM) * (p.coutp / bn);
   int G = num_cu < T ? num_cu : T;
   G = G / 8 * 8;
-  const size_t lds = GW_NST * GW_SLOT + ((p.flags & EPI_AFFINE) ? 8 * (size_t)p.coutp : 0);
+  const size_t lds = GW_NST * GW_SLOT + 8 * (size_t)p.coutp + (p.in_mean ? 8 * (size_t)p.kp : 0);
+  if (p.in_mean || p.kh > 1) {
+    // operand variants (GS_PRO / GS_TAPS): wave-specialised only
+    const int T2 = ((M + 191) / 192) * (p.coutp / 256);
+    int G2 = num_cu < T2 ? num_cu : T2;
+    G2 = G2 >= 8 ? G2 / 8 * 8 : G2;
+    const int T3 = ((M + 255) / 256) * (p.coutp / 192);
+    int G3 = num_cu < T3 ? num_cu : T3;
+    G3 = G3 >= 8 ? G3 / 8 * 8 : G3;
+    if (p.in_mean) {
+      if (p.flags & EPI_RES)
+        hipLaunchKernelGGL((gemm1x1_ws<256, true, 192, 0, GS_PRO>), dim3(G2), dim3(GS_NT), lds, s, p);
+      else if (bn == 192)
+        hipLaunchKernelGGL((gemm1x1_ws<192, false, 256, 0, GS_PRO>), dim3(G3), dim3(GS_NT), lds, s, p);
+      else
+        hipLaunchKernelGGL((gemm1x1_ws<256, false, 192, 0, GS_PRO>), dim3(G2), dim3(GS_NT), lds, s, p);
+    } else {
+      if (bn == 192)
+        hipLaunchKernelGGL((gemm1x1_ws<192, false, 256, 0, GS_TAPS>), dim3(G3), dim3(GS_NT), lds, s, p);
+      else
+        hipLaunchKernelGGL((gemm1x1_ws<256, false, 192, 0, GS_TAPS>), dim3(G2), dim3(GS_NT), lds, s, p);
+    }
+    return hipGetLastError();
+  }
   // wave-specialised by default (4-11 % faster per launch; the 256-wide tiles
   // with 192 pixels so the compute waves fit the 12-wave register cap);
   // VOXEMB_GEMM_VAR=-1 selects gemm1x1_wide
