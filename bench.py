@@ -49,7 +49,7 @@ def _kernel_name(tag, dt):
     if tag & (1 << 24):
         return "bneck_fused"
     if tag & (1 << 23):
-        return "stem_conv1"
+        return "conv1x1_smallk" if tag & (1 << 19) else "stem_conv1"
     if tag & (1 << 22):
         return f"split_chain<{(tag >> 4) & 15}, {(tag >> 8) & 15}>"
     if tag & (1 << 21):
@@ -79,9 +79,11 @@ def pmc_traffic(kernel):
     except (OSError, ValueError):
         return None
     base = kernel.split("<")[0]
+    # the stats pool runs as stats_pool_col (short time axis) or stats_pool_k
+    bases = {"stats_pool_k", "stats_pool_col"} if base.startswith("stats_pool") else {base}
     tot = disp = 0.0
     for name, r in summ.items():
-        if name.split("::")[-1].split("<")[0] == base and "hbm_bytes" in r:
+        if name.split("::")[-1].split("<")[0] in bases and "hbm_bytes" in r:
             n = r["mean"].get("dispatches", 1)
             tot += r["hbm_bytes"] * n
             disp += n

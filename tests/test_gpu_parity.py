@@ -529,7 +529,7 @@ def test_gemm_ws_prologue_bitwise(weights, name, F, T, N, monkeypatch):
     assert np.array_equal(got, ref)
 
 
-@pytest.mark.parametrize("F,T,N", [(80, 200, 64), (40, 320, 5), (40, 37, 3)])
+@pytest.mark.parametrize("F,T,N", [(80, 200, 64), (40, 320, 7), (40, 37, 48)])
 def test_gemm_ws_taps_bitwise(weights, F, T, N, monkeypatch):
     """TDNN dilated convs (k5d1, k3d2, k3d3) on gemm1x1_ws<.., GS_TAPS>: every
     tap's rows gathered by the loader waves, zero rows outside the utterance

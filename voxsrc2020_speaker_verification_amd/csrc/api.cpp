@@ -255,6 +255,8 @@ struct vox_model {
   bool no_conv3 = false;
   bool no_gemm_pro = false;    // VOXEMB_NO_GEMM_PRO=1: prologue 1x1 convs off the LDS-DMA GEMMs
   bool no_gemm_taps = false;   // VOXEMB_NO_GEMM_TAPS=1: TDNN dilated convs off gemm1x1_ws
+  bool no_smallk = false;      // VOXEMB_NO_SMALLK=1: DPN 10-channel 1x1s on the generic conv
+  int pro_min_cout = 192;      // VOXEMB_PRO_MIN_COUT: narrowest prologue 1x1 on gemm1x1_ws
   int num_cu = 256;            // compute units (persistent grids)
   int gemm_var = 0;            // VOXEMB_GEMM_VAR: gemm1x1_pipe variant (A/B experiments)
   int gemm_min_k = 128;        // VOXEMB_GEMM_MIN_K: smallest K routed to the LDS GEMMs (the K = 128
@@ -665,7 +667,8 @@ static void emit_conv(Builder& B, const ConvW& cw, Act x, const void* x2, int ld
   // that the prologue zeroes, slots carry slack for the last row)
   if (op.type != 18 && op.type != 21 && B.m->dt == BF16 && dt_override != F32 && in_mean &&
       cw.wblk && !B.m->no_gemm_wide && !B.m->no_gemm_pro && !(flags & EPI_PARTIAL) && ph == 0 &&
-      pw == 0 && cw.kh == 1 && cw.kw == 1 && cw.groups == 1 && cw.cout >= 192 && cw.cout % 8 == 0 &&
+      pw == 0 && cw.kh == 1 && cw.kw == 1 && cw.groups == 1 && cw.cout >= B.m->pro_min_cout &&
+      cw.cout % 8 == 0 &&
       ldy % 8 == 0 && (ysplit >= (1 << 30) || (ysplit % 8 == 0 && ldy2 % 8 == 0)) &&
       (!res || ldr % 8 == 0) && x.ld % 8 == 0) {
     ConvParams q = p;
@@ -769,6 +772,10 @@ static void emit_conv(Builder& B, const ConvW& cw, Act x, const void* x2, int ld
       }
     }
   }
+  // 10-channel input (DPN68 stem output) with the prologue: vector-ALU kernel
+  if (op.type == 0 && B.m->dt == BF16 && dt_override != F32 && in_mean && !B.m->no_smallk &&
+      conv1x1_smallk_ok(p))
+    op.type = 27;
   if (dt_override == F32) op.type = 5;
   const double es = dt_override == F32 ? 4.0 : (double)es_of(B.m);
   op.flops = 2.0 * M * cw.cout * cw.groups * (double)cw.kh * cw.kw * cw.cin;
@@ -1483,6 +1490,7 @@ static hipError_t run_op(vox_model* m, const Op& op, hipStream_t s) {
     case 23: return launch_conv3_win(op.cp, m->num_cu, s);
     case 25: return launch_conv3_rw(op.cp, m->num_cu, s);
     case 26: return launch_conv3_utt(op.cp, m->num_cu, s);
+    case 27: return launch_conv1x1_smallk(op.cp, s);
     case 15: return launch_convert_bf16(op.src, (float*)op.dst, op.count, s);
     case 16: return launch_att_bias_tanh((float*)op.dst, (const float*)op.src, op.N, op.H, op.W, op.C, s);
     case 17:
@@ -1561,6 +1569,8 @@ extern "C" int vox_load_blob(const void* blob, size_t nbytes, int device, int pr
   if (const char* e = std::getenv("VOXEMB_NO_CONV3")) m->no_conv3 = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_NO_GEMM_PRO")) m->no_gemm_pro = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_NO_GEMM_TAPS")) m->no_gemm_taps = std::atoi(e) != 0;
+  if (const char* e = std::getenv("VOXEMB_NO_SMALLK")) m->no_smallk = std::atoi(e) != 0;
+  if (const char* e = std::getenv("VOXEMB_PRO_MIN_COUT")) m->pro_min_cout = std::atoi(e);
   if (const char* e = std::getenv("VOXEMB_GEMM_VAR")) m->gemm_var = std::atoi(e);
   if (const char* e = std::getenv("VOXEMB_GEMM_MIN_K")) m->gemm_min_k = std::atoi(e);
   if (const char* e = std::getenv("VOXEMB_NO_CHAIN")) m->no_chain = std::atoi(e) != 0;
@@ -1736,6 +1746,8 @@ extern "C" int vox_profile(vox_model* m, const float* d_x, int n, int t, int f, 
         tag |= (o.cl.wco << 4) | (o.cl.wpx << 8) | (1 << 22);
       else if (o.type == 11)
         tag |= (1 << 23);
+      else if (o.type == 27)
+        tag |= (1 << 23) | (1 << 19);
       else if (o.type == 12)
         tag |= (1 << 24);
       else if (o.type == 13)
@@ -1788,12 +1800,14 @@ extern "C" int vox_plan_describe(vox_model* m, const float* d_x, int n, int t, i
   static const char* tn[] = {"igemm", "reduce", "pool", "avgpool", "convert", "igemm32", "bnrelu",
                              "win", "rr", "gemm", "chain", "stem", "bneck", "chainrows", "splits2",
                              "cvt16", "atttanh", "attpool", "gemmpipe", "gconv", "conv3pipe",
-                             "gemmwide", "s2fused", "conv3win", "chainfused", "conv3rw", "conv3utt"};
+                             "gemmwide", "s2fused", "conv3win", "chainfused", "conv3rw", "conv3utt",
+                             "smallk"};
   for (const Op& o : m->plan) {
     char line[256];
     const ConvParams& p = o.cp;
     if (o.type == 0 || o.type == 5 || o.type == 7 || o.type == 8 || o.type == 9 || o.type == 18 ||
-        o.type == 20 || o.type == 21 || o.type == 23 || o.type == 25 || o.type == 26)
+        o.type == 20 || o.type == 21 || o.type == 23 || o.type == 25 || o.type == 26 ||
+        o.type == 27)
       std::snprintf(line, sizeof(line),
                     "%s wco=%d wpx=%d s=%d N=%d H=%d W=%d Cin=%d Ho=%d Wo=%d Cout=%d k=%dx%d st=%d "
                     "g=%d flags=%d x2=%d pro=%d flops=%.4g bytes=%.4g\n",

@@ -688,7 +688,7 @@ int gemm_wide_bn(const ConvParams& p) {
   if (p.Cout % 256 == 0) bn = 256;
   else if (p.Cout % 192 == 0 && !(p.flags & EPI_RES)) bn = 192;
   // DPN prologue convs: partial last cout tile (the weights hold 256-row multiples)
-  else if (p.in_mean && p.Cout >= 192) bn = 256;
+  else if (p.in_mean && p.Cout >= 128) bn = 256;
   if (!bn || p.Cout > 2048) return 0;
   if ((p.flags & EPI_RES) && (!p.res || p.ldr % 8)) return 0;
   const int T = ((M + GW_BM - 1) / GW_BM) * (p.Cout / bn);

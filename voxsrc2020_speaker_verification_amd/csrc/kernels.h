@@ -183,6 +183,10 @@ int gconv_rs(const GconvParams& p);
 int gconv_lds(const GconvParams& p);
 hipError_t launch_gconv(const GconvParams& p, hipStream_t s);
 
+// DPN68's 10-channel 1x1 convs with the BN+ReLU prologue (kernels.hip)
+int conv1x1_smallk_ok(const ConvParams& p);
+hipError_t launch_conv1x1_smallk(const ConvParams& p, hipStream_t s);
+
 hipError_t launch_splitk_reduce(const float* partial, int S, int M, int coutp, int cout,
                                 const float* mean, const float* inv, int flags,
                                 float* out, int ldo, hipStream_t s);

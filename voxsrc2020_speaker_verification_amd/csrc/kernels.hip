@@ -1384,71 +1384,70 @@ __global__ __launch_bounds__(64 * TS) void stats_pool_k(const T* __restrict__ x,
 // a row), both passes of tf.nn.moments from those registers, no LDS and no
 // barrier: every byte is read once with H loads in flight per thread.
 // Sequential summation over h (a fixed order per column, batch-independent).
-template <int HM>
+template <int HM, int VN>
 __global__ __launch_bounds__(256) void stats_pool_col(const bf16_t* __restrict__ x, int N, int H,
                                                       int W, int C,
                                                       const float* __restrict__ mean,
                                                       const float* __restrict__ inv,
                                                       float* __restrict__ out) {
-  const int chunks = C / 8;
+  typedef __bf16 bfv __attribute__((ext_vector_type(VN)));
+  typedef unsigned uv __attribute__((ext_vector_type(VN / 2)));
+  typedef float fv __attribute__((ext_vector_type(VN)));
+  const int chunks = C / VN;
   const int64_t gcol = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (gcol >= (int64_t)N * W * chunks) return;
   const int n = (int)(gcol / ((int64_t)W * chunks));
   const int r = (int)(gcol - (int64_t)n * W * chunks);
   const int w = r / chunks, ch = r - (r / chunks) * chunks;
-  const bf16_t* base = x + ((size_t)n * H * W + w) * C + (size_t)ch * 8;
+  const bf16_t* base = x + ((size_t)n * H * W + w) * C + (size_t)ch * VN;
   const size_t rowstride = (size_t)W * C;
-  bf16x8 v[HM];
+  uv v[HM];
 #pragma unroll
   for (int h = 0; h < HM; ++h)
-    if (h < H) v[h] = ld16(base + (size_t)h * rowstride);
-  float s[8], q[8];
+    if (h < H) v[h] = *reinterpret_cast<const uv*>(base + (size_t)h * rowstride);
+  float s[VN], q[VN];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) s[e] = q[e] = 0.f;
+  for (int e = 0; e < VN; ++e) s[e] = q[e] = 0.f;
 #pragma unroll
   for (int h = 0; h < HM; ++h)
     if (h < H) {
+      const bfv b = __builtin_bit_cast(bfv, v[h]);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) s[e] += (float)v[h][e];
+      for (int e = 0; e < VN; ++e) s[e] += (float)b[e];
     }
-  float mu[8];
+  float mu[VN];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) mu[e] = s[e] / (float)H;
-  // the rows stay packed bf16 between the passes (4 VGPRs each): without this the
-  // compiler keeps every converted float of pass 1 live for pass 2 (256 VGPRs)
+  for (int e = 0; e < VN; ++e) mu[e] = s[e] / (float)H;
+  // the rows stay packed bf16 between the passes: without this the compiler
+  // keeps every converted float of pass 1 live for pass 2
 #pragma unroll
-  for (int h = 0; h < HM; ++h) {
-    vu32x4 t = __builtin_bit_cast(vu32x4, v[h]);
-    asm volatile("" : "+v"(t));
-    v[h] = __builtin_bit_cast(bf16x8, t);
-  }
+  for (int h = 0; h < HM; ++h) asm volatile("" : "+v"(v[h]));
 #pragma unroll
   for (int h = 0; h < HM; ++h)
     if (h < H) {
+      const bfv b = __builtin_bit_cast(bfv, v[h]);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float d = (float)v[h][e] - mu[e];
+      for (int e = 0; e < VN; ++e) {
+        const float d = (float)b[e] - mu[e];
         q[e] += d * d;
       }
     }
-  float* o = out + (size_t)n * W * 2 * C + (size_t)w * 2 * C + (size_t)ch * 8;
-  f32x4 om[2], os[2];
+  float* o = out + (size_t)n * W * 2 * C + (size_t)w * 2 * C + (size_t)ch * VN;
+  fv om, os;
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
+  for (int e = 0; e < VN; ++e) {
     float sd = sqrtf(q[e] / (float)H + 1e-5f);
     float m = mu[e];
-    const int fm = w * 2 * C + ch * 8 + e, fs = fm + C;
+    const int fm = w * 2 * C + ch * VN + e, fs = fm + C;
     if (mean) {
       m = (m - mean[fm]) * inv[fm];
       sd = (sd - mean[fs]) * inv[fs];
     }
-    om[e >> 2][e & 3] = m;
-    os[e >> 2][e & 3] = sd;
+    om[e] = m;
+    os[e] = sd;
   }
-  *reinterpret_cast<f32x4*>(o) = om[0];
-  *reinterpret_cast<f32x4*>(o + 4) = om[1];
-  *reinterpret_cast<f32x4*>(o + C) = os[0];
-  *reinterpret_cast<f32x4*>(o + C + 4) = os[1];
+  *reinterpret_cast<fv*>(o) = om;
+  *reinterpret_cast<fv*>(o + C) = os;
 }
 
 template <typename T, int VN>
@@ -1457,13 +1456,15 @@ static hipError_t stats_pool_ts(const T* x, int N, int H, int W, int C, const fl
   const int64_t cols = (int64_t)N * W * (C / VN);
   if constexpr (sizeof(T) == 2 && VN == 8) {
     if (H <= 32) {
-      const unsigned b = (unsigned)((cols + 255) / 256);
+      // 4 channels (8 B) per thread: the rows of a column in 2 VGPRs each, so
+      // the whole utterance axis is in flight at 8 waves per SIMD
+      const unsigned b = (unsigned)((cols * 2 + 255) / 256);
       if (H <= 16)
-        hipLaunchKernelGGL((stats_pool_col<16>), dim3(b), dim3(256), 0, s, x, N, H, W, C, mean, inv, out);
+        hipLaunchKernelGGL((stats_pool_col<16, 4>), dim3(b), dim3(256), 0, s, x, N, H, W, C, mean, inv, out);
       else if (H <= 25)   // T = 200 at layer 4 (the headline)
-        hipLaunchKernelGGL((stats_pool_col<25>), dim3(b), dim3(256), 0, s, x, N, H, W, C, mean, inv, out);
+        hipLaunchKernelGGL((stats_pool_col<25, 4>), dim3(b), dim3(256), 0, s, x, N, H, W, C, mean, inv, out);
       else
-        hipLaunchKernelGGL((stats_pool_col<32>), dim3(b), dim3(256), 0, s, x, N, H, W, C, mean, inv, out);
+        hipLaunchKernelGGL((stats_pool_col<32, 4>), dim3(b), dim3(256), 0, s, x, N, H, W, C, mean, inv, out);
       return hipGetLastError();
     }
   }
@@ -1722,4 +1723,70 @@ hipError_t launch_att_pool(DType t, const void* x, const float* lg, int N, int H
   return hipGetLastError();
 }
 
+}  // namespace vox
+
+namespace vox {
+// ----------------------------------------------------------------------------
+// Small-K 1x1 conv with the BN + ReLU input prologue (DPN68's first projection
+// and 1x1a read the 10-channel stem output, dpn_model.py:40-45,111-130): too
+// narrow a K for the MFMA paths (one 32-step of which 22 are zero).  Thread =
+// (pixel, 8 output channels): x -> relu((x - m) * inv) rounded to bf16 (the
+// MFMA operand the other paths feed), products with the bf16 weights exact in
+// fp32, summed over k in order, one bf16 rounding of the sum.  Weights
+// [Cout][kp] (the generic layout), read at wave-uniform addresses.
+template <int K>
+__global__ __launch_bounds__(256) void conv1x1_smallk(ConvParams p) {
+  // thread = pixel; the weights (as fp32) and the prologue BN in LDS, read at
+  // wave-uniform addresses (broadcast); output chunks of 8 channels in order
+  __shared__ float ws[256 * K];
+  __shared__ float bm[K], bi[K];
+  const int tid = threadIdx.x;
+  const bf16_t* __restrict__ Wt = reinterpret_cast<const bf16_t*>(p.w);
+  for (int i = tid; i < p.Cout * K; i += 256) ws[i] = (float)Wt[(size_t)(i / K) * p.kp + i % K];
+  if (tid < K) {
+    bm[tid] = p.in_mean ? p.in_mean[tid] : 0.f;
+    bi[tid] = p.in_mean ? p.in_inv[tid] : 1.f;
+  }
+  __syncthreads();
+  const int64_t pix = (int64_t)blockIdx.x * 256 + tid;
+  if (pix >= (int64_t)p.N * p.H * p.W) return;
+  const bf16_t* __restrict__ X = reinterpret_cast<const bf16_t*>(p.x) + pix * p.ldx;
+  float xv[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    float v = (float)X[k];
+    if (p.in_mean) v = fmaxf((v - bm[k]) * bi[k], 0.f);
+    xv[k] = (float)(bf16_t)v;   // the bf16 operand the MFMA paths feed
+  }
+  bf16_t* Y = reinterpret_cast<bf16_t*>(p.y);
+  bf16_t* Y2 = reinterpret_cast<bf16_t*>(p.y2);
+  for (int co = 0; co < p.Cout; co += 8) {
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float* w = ws + (co + e) * K;
+      float acc = 0.f;
+#pragma unroll
+      for (int k = 0; k < K; ++k) acc = fmaf(xv[k], w[k], acc);
+      o[e] = (bf16_t)acc;
+    }
+    bf16_t* dst = co < p.ysplit ? Y + pix * p.ldy + co : Y2 + pix * p.ldy2 + (co - p.ysplit);
+    *reinterpret_cast<uint4*>(dst) = __builtin_bit_cast(uint4, o);
+  }
+}
+
+int conv1x1_smallk_ok(const ConvParams& p) {
+  return p.kh == 1 && p.kw == 1 && p.sh == 1 && p.sw == 1 && p.ph == 0 && p.pw == 0 &&
+         p.groups == 1 && p.Cin == 10 && p.Cout % 8 == 0 && p.Cout <= 256 && p.flags == 0 &&
+         !p.x2 && !p.res &&
+         p.ldy % 8 == 0 && (p.ysplit >= (1 << 30) || (p.ysplit % 8 == 0 && p.ldy2 % 8 == 0)) &&
+         p.Ho == p.H && p.Wo == p.W;
+}
+
+hipError_t launch_conv1x1_smallk(const ConvParams& p, hipStream_t s) {
+  if (!conv1x1_smallk_ok(p)) return hipErrorInvalidValue;
+  const int64_t n = (int64_t)p.N * p.H * p.W;
+  hipLaunchKernelGGL((conv1x1_smallk<10>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
 }  // namespace vox
