@@ -36,7 +36,9 @@ def _kernel_name(tag, dt):
         return "gemm1x1_ws" if tag & (1 << 17) else "gemm1x1_wide"
     if tag & (1 << 29):
         if tag & (1 << 18):
-            return "conv3x3_utt" if tag & (1 << 17) else "conv3x3_rw"
+            if tag & (1 << 17):
+                return "conv3x3_utt"
+            return "conv3x3_s2r" if tag & (1 << 19) else "conv3x3_rw"
         return "conv3x3_win" if tag & (1 << 19) else "conv3x3_pipe"
     if tag & (1 << 28):
         return "gconv3x3_rows"

@@ -551,3 +551,26 @@ def test_gemm_ws_taps_bitwise(weights, F, T, N, monkeypatch):
         assert not any(l.startswith("gemmwide") and "k=3x1" in l
                        for l in ex.describe(torch.from_numpy(x).cuda()))
     assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("name,F,T,N", [("res2net50_w24_s4_c32", 80, 200, 16),
+                                        ("res2net50_w24_s4_c32", 80, 123, 7),
+                                        ("res2net50_w24_s4_c32", 80, 27, 1),
+                                        ("res2net101_w24_s4_c32_att", 80, 64, 3)])
+def test_conv3_s2r_bitwise_pipe(weights, name, F, T, N, monkeypatch):
+    """The register-weight stride-2 3x3 (layer-3 block 0: 3-row output tiles,
+    the 7-row input window staged once with odd columns before even ones,
+    partial last tile, odd input heights) gives the same bits as
+    conv3x3_pipe's im2col gather."""
+    import torch
+    from voxsrc2020_speaker_verification_amd import synth
+    spec, t, blob = weights(name, F)
+    x = synth.make_features(N, T, F, seed=53)
+    with _extractor(blob, "bf16") as ex:
+        got = ex.run(x)
+        assert sum(l.startswith("conv3s2r") for l in ex.describe(torch.from_numpy(x).cuda())) == 3
+    monkeypatch.setenv("VOXEMB_NO_CONV3_S2R", "1")
+    with _extractor(blob, "bf16") as ex:
+        ref = ex.run(x)
+        assert not any(l.startswith("conv3s2r") for l in ex.describe(torch.from_numpy(x).cuda()))
+    assert np.array_equal(got, ref)

@@ -23,6 +23,7 @@ SOURCES = [
     ("conv3w.hip", ["-O3"]),
     ("conv3r.hip", ["-O3"]),
     ("conv3u.hip", ["-O3"]),
+    ("conv3s.hip", ["-O3"]),
     ("fbank.hip", ["-O3"]),
     ("api.cpp", ["-O2"]),
     ("kaldi_host.cpp", ["-O2", "-ffp-contract=off"]),

@@ -251,6 +251,7 @@ struct vox_model {
   bool no_conv3_win = true;
   bool no_conv3_rw = false;    // VOXEMB_NO_CONV3_RW=1: conv3x3_pipe for the w = 96 stride-1 branches
   bool no_conv3_utt = false;   // VOXEMB_NO_CONV3_UTT=1: conv3x3_pipe for the w = 192 stride-1 branches
+  bool no_conv3_s2r = false;   // VOXEMB_NO_CONV3_S2R=1: conv3x3_pipe for the w = 96 stride-2 branches
   bool no_gconv = false;       // VOXEMB_NO_GCONV=1: grouped 3x3 on the generic implicit GEMM
   bool no_conv3 = false;
   bool no_gemm_pro = false;    // VOXEMB_NO_GEMM_PRO=1: prologue 1x1 convs off the LDS-DMA GEMMs
@@ -1277,6 +1278,8 @@ static int build_res2net(Builder& B, const float* x, int n, int t, float* out) {
           else if (ok && !m->no_conv3_rw && conv3_rw_ok(p)) op.type = 25;
           // w = 192: one utterance band's window staged once, weights streamed (conv3u.hip)
           else if (ok && !m->no_conv3_utt && conv3_utt_ok(p)) op.type = 26;
+          // stride 2, w = 96: register weights, 3-row window tiles (conv3s.hip)
+          else if (ok && !m->no_conv3_s2r && conv3_s2r_ok(p)) op.type = 28;
           op.flops = 2.0 * n * Ho * Wo * 9.0 * br.cin * br.cout;
           op.bytes = (double)es * ((double)n * H * W * br.cin +
                                    (double)n * Ho * Wo * br.cout * (z ? 3.0 : 1.0));
@@ -1491,6 +1494,7 @@ static hipError_t run_op(vox_model* m, const Op& op, hipStream_t s) {
     case 25: return launch_conv3_rw(op.cp, m->num_cu, s);
     case 26: return launch_conv3_utt(op.cp, m->num_cu, s);
     case 27: return launch_conv1x1_smallk(op.cp, s);
+    case 28: return launch_conv3_s2r(op.cp, m->num_cu, s);
     case 15: return launch_convert_bf16(op.src, (float*)op.dst, op.count, s);
     case 16: return launch_att_bias_tanh((float*)op.dst, (const float*)op.src, op.N, op.H, op.W, op.C, s);
     case 17:
@@ -1583,6 +1587,7 @@ extern "C" int vox_load_blob(const void* blob, size_t nbytes, int device, int pr
   if (const char* e = std::getenv("VOXEMB_CONV3_WIN")) m->no_conv3_win = std::atoi(e) == 0;
   if (const char* e = std::getenv("VOXEMB_NO_CONV3_RW")) m->no_conv3_rw = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_NO_CONV3_UTT")) m->no_conv3_utt = std::atoi(e) != 0;
+  if (const char* e = std::getenv("VOXEMB_NO_CONV3_S2R")) m->no_conv3_s2r = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_BNECK_NSEG")) m->bneck_nseg = std::atoi(e);
   if (const char* e = std::getenv("VOXEMB_BNECK_DBG")) m->bneck_dbg = std::atoi(e);
   if (const char* e = std::getenv("VOXEMB_CHAIN_R")) m->chain_r = std::atoi(e);
@@ -1770,6 +1775,8 @@ extern "C" int vox_profile(vox_model* m, const float* d_x, int n, int t, int f, 
         tag |= (1 << 29) | (1 << 18);
       else if (o.type == 26)
         tag |= (1 << 29) | (1 << 18) | (1 << 17);
+      else if (o.type == 28)
+        tag |= (1 << 29) | (1 << 18) | (1 << 19);
       else if (o.type == 8)
         tag |= (o.cl.wco << 4) | (o.cl.wpx << 8) | (((o.cp.cinp + 31) / 32) << 16) | (1 << 20);
       else if (o.type == 0 || o.type == 5)
@@ -1801,13 +1808,13 @@ extern "C" int vox_plan_describe(vox_model* m, const float* d_x, int n, int t, i
                              "win", "rr", "gemm", "chain", "stem", "bneck", "chainrows", "splits2",
                              "cvt16", "atttanh", "attpool", "gemmpipe", "gconv", "conv3pipe",
                              "gemmwide", "s2fused", "conv3win", "chainfused", "conv3rw", "conv3utt",
-                             "smallk"};
+                             "smallk", "conv3s2r"};
   for (const Op& o : m->plan) {
     char line[256];
     const ConvParams& p = o.cp;
     if (o.type == 0 || o.type == 5 || o.type == 7 || o.type == 8 || o.type == 9 || o.type == 18 ||
         o.type == 20 || o.type == 21 || o.type == 23 || o.type == 25 || o.type == 26 ||
-        o.type == 27)
+        o.type == 27 || o.type == 28)
       std::snprintf(line, sizeof(line),
                     "%s wco=%d wpx=%d s=%d N=%d H=%d W=%d Cin=%d Ho=%d Wo=%d Cout=%d k=%dx%d st=%d "
                     "g=%d flags=%d x2=%d pro=%d flops=%.4g bytes=%.4g\n",

@@ -136,6 +136,11 @@ hipError_t launch_conv3_rw(const ConvParams& p, int num_cu, hipStream_t s);
 // Utterance-band window 3x3 conv for the w = 192 stride-1 branches (conv3u.hip)
 int conv3_utt_ok(const ConvParams& p);
 hipError_t launch_conv3_utt(const ConvParams& p, int num_cu, hipStream_t s);
+// Register-weight stride-2 3x3 (conv3s.hip): w = 96 branches of a stride-2
+// block at 40 -> 20 columns, output tiles of 3 rows with their input window
+// staged once in LDS.
+int conv3_s2r_ok(const ConvParams& p);
+hipError_t launch_conv3_s2r(const ConvParams& p, int num_cu, hipStream_t s);
 int conv3_win_ok(const ConvParams& p);
 hipError_t launch_conv3_win(const ConvParams& p, int num_cu, hipStream_t s);
 // Wide-tile variant (gemm_wide.hip): 256 x BN tiles, BN = 256 (Cout % 256 == 0)

@@ -1523,6 +1523,7 @@ __global__ __launch_bounds__(256) void avgpool3s2_k(const T* __restrict__ x, int
 }
 
 // bf16, C % 8 == 0: 8 channels per thread with 16-byte loads/stores (same sum order)
+__device__ uint4 g_pool_zero[1] = {};
 __global__ __launch_bounds__(256) void avgpool3s2_v8(const bf16_t* __restrict__ x, int ldx, int N,
                                                      int H, int W, int C8, bf16_t* __restrict__ y,
                                                      int ldy, int Ho, int Wo) {
@@ -1536,16 +1537,23 @@ __global__ __launch_bounds__(256) void avgpool3s2_v8(const bf16_t* __restrict__ 
   const int wo = (int)(pix - nh * (unsigned)Wo);
   const int n = (int)(nh / (unsigned)Ho);
   const int ho = (int)(nh - (unsigned)n * (unsigned)Ho);
-  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int ky = 0; ky < 3; ++ky) {
-    const int hi = 2 * ho - 1 + ky;
-    if (hi < 0 || hi >= H) continue;
-    for (int kx = 0; kx < 3; ++kx) {
-      const int wi = 2 * wo - 1 + kx;
-      if (wi < 0 || wi >= W) continue;
-      const bf16x8 v = ld16(x + (((size_t)n * H + hi) * W + wi) * ldx + c);
+  // all nine taps requested at once (padding taps read a zero line and add an
+  // exact +0: the same sums in the same order as skipping them)
+  bf16x8 v[9];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) s[e] += (float)v[e];
+  for (int t = 0; t < 9; ++t) {
+    const int hi = 2 * ho - 1 + t / 3, wi = 2 * wo - 1 + t % 3;
+    const bool ok = hi >= 0 && hi < H && wi >= 0 && wi < W;
+    v[t] = ld16(ok ? x + (((size_t)n * H + hi) * W + wi) * ldx + c
+                   : reinterpret_cast<const bf16_t*>(g_pool_zero));
+  }
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int hi = 2 * ho - 1 + t / 3, wi = 2 * wo - 1 + t % 3;
+    if (hi >= 0 && hi < H && wi >= 0 && wi < W) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s[e] += (float)v[t][e];
     }
   }
   bf16x8 o;
