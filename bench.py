@@ -67,18 +67,32 @@ def _kernel_name(tag, dt):
     return {1: "stats_pool_k", 2: "splitk_reduce", 3: "other"}.get(kind, "other")
 
 
+# committed rocprofv3 PMC summaries (tools/pmc_summary.py), one per profiled
+# configuration: (model, feat_dim, frames, batch, precision) -> file
+PMC_SUMMARIES = {
+    ("res2net50_w24_s4_c32", 80, 200, 256, "bf16"): "pmc_summary.json",
+    ("tdnn", 80, 200, 64, "bf16"): "pmc_summary_tdnn.json",
+    ("dpn68", 80, 600, 64, "bf16"): "pmc_summary_dpn68.json",
+}
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_summary.json")
 
 
-def pmc_traffic(kernel):
+def _load_pmc(path):
+    try:
+        with open(path) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return None
+
+
+def pmc_traffic(kernel, summ=None):
     """HBM bytes per dispatch of `kernel` from the committed rocprofv3 PMC
     summary (tools/pmc_summary.py: FETCH_SIZE x2 + WRITE_SIZE, the gfx950
     corrections of MI355X_MICROARCH.md "HBM"), averaged over the template
     instances of the same kernel by dispatch count; None if not profiled."""
-    try:
-        with open(PMC_SUMMARY) as f:
-            summ = json.load(f)
-    except (OSError, ValueError):
+    if summ is None:
+        summ = _load_pmc(PMC_SUMMARY)
+    if summ is None:
         return None
     base = kernel.split("<")[0]
     # the stats pool runs as stats_pool_col (short time axis) or stats_pool_k
@@ -90,6 +104,26 @@ def pmc_traffic(kernel):
             tot += r["hbm_bytes"] * n
             disp += n
     return tot / disp if disp else None
+
+
+def pmc_mfma_busy(summ):
+    """Conv-stack MFMA utilisation from the PMC summary's MFMA-busy pass:
+    SQ_VALU_MFMA_BUSY_CYCLES summed over the kernels with MFMA work against
+    1024 SIMDs x their GRBM_GUI_ACTIVE/8 cycles, weighted by dispatches (one
+    profiled forward's worth of launches)."""
+    if not summ:
+        return None
+    busy = cyc = 0.0
+    per = {}
+    for name, r in summ.items():
+        m = r.get("mean", {})
+        if not m.get("SQ_VALU_MFMA_BUSY_CYCLES") or not r.get("gui_cycles"):
+            continue
+        n = m.get("dispatches", 1)
+        busy += m["SQ_VALU_MFMA_BUSY_CYCLES"] * n
+        cyc += 1024.0 * r["gui_cycles"] * n
+        per[name.split("(")[0]] = round(r["mfma_busy_frac"], 4)
+    return {"conv_stack_mfma_busy": round(busy / cyc, 4) if cyc else None, "per_kernel": per}
 
 
 def weights_blob(model, feat_dim, cache_dir):
@@ -253,9 +287,9 @@ def main():
     pool = groups.get("stats_pool_k")
     # the committed PMC summary was collected on the default workload only; on any
     # other model/shape its per-launch bytes belong to different launches
-    pmc_ok = ((args.model, F, T, B, args.precision)
-              == ("res2net50_w24_s4_c32", 80, 200, 256, "bf16"))
-    traffic = pmc_traffic if pmc_ok else (lambda k: None)
+    pmc_file = PMC_SUMMARIES.get((args.model, F, T, B, args.precision))
+    summ = _load_pmc(os.path.join(ROOT, "profiles", pmc_file)) if pmc_file else None
+    traffic = (lambda k: pmc_traffic(k, summ)) if summ else (lambda k: None)
     if t_hbm >= t_mfma:
         roof = {"bound": "hbm", "kernel": dom_name, "launches_per_step": dom["n"],
                 "achieved": round(ach_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
@@ -266,7 +300,7 @@ def main():
                 "frac": round(ach / peak, 4)}
     roof.update({
         "traffic": traffic(dom_name),
-        "traffic_unit": "HBM bytes per launch (rocprofv3 PMC, profiles/pmc_summary.json)",
+        "traffic_unit": f"HBM bytes per launch (rocprofv3 PMC, profiles/{pmc_file})",
         "algorithmic_bytes_per_launch": dom["bytes"] / dom["n"],
         "avg_launch_us": round(dom["ms"] / dom["n"] * 1e3, 2),
         "flop_per_launch": dom["flops"] / dom["n"],
@@ -278,6 +312,8 @@ def main():
         "conv_stack": {"achieved_tflops": round(conv_fl / (conv_ms * 1e-3) / 1e12, 2),
                        "frac": round(conv_fl / (conv_ms * 1e-3) / 1e12 / peak, 4),
                        "ms": round(conv_ms, 3), "flop": conv_fl},
+        "mfma_pmc": (dict(pmc_mfma_busy(summ) or {}, source=f"profiles/{pmc_file}")
+                     if summ else None),
         "forward_ms_profiled": round(fwd_ms, 3),
         "kernels": {k: {"n": v["n"], "ms": round(v["ms"], 4),
                         "tflops": round(v["flops"] / max(v["ms"], 1e-9) / 1e9, 2) if v["flops"] else None,
