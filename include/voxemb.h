@@ -121,7 +121,7 @@ typedef struct vox_fbank_opts {
   int num_mel_bins;               /* Kaldi default 23; 80 / 40 in conf/fbank{80,40}.conf */
   float low_freq;                 /* 20 */
   float high_freq;                /* 0: Nyquist (negative: offset from Nyquist) */
-  uint64_t seed;                  /* dither noise = f(seed, frame index, sample index) */
+  uint64_t seed;                  /* dither noise = f(seed, utterance key, frame, sample) */
 } vox_fbank_opts;
 void vox_fbank_default_opts(vox_fbank_opts* o);
 /* Frames of an utterance of num_samples samples (snip_edges), or < 0. */
@@ -134,11 +134,31 @@ int64_t vox_fbank_num_frames(int64_t num_samples, const vox_fbank_opts* o);
 int vox_fbank_device(const float* d_wav, const int64_t* d_samp_off, const int64_t* d_frame_off,
                      int n_utt, int64_t total_frames, const vox_fbank_opts* o, float* d_out,
                      void* stream);
+/* As vox_fbank_device, with d_utt_key: device uint64[n_utt] per-utterance
+ * dither keys (e.g. a hash of the utterance id), so every utterance draws its
+ * own noise -- as Kaldi's per-utterance RandomState does -- while the result
+ * stays independent of batch composition.  d_utt_key == NULL is
+ * vox_fbank_device (noise a function of seed, frame and sample only). */
+int vox_fbank_device_keyed(const float* d_wav, const int64_t* d_samp_off,
+                           const int64_t* d_frame_off, const uint64_t* d_utt_key, int n_utt,
+                           int64_t total_frames, const vox_fbank_opts* o, float* d_out,
+                           void* stream);
 /* Sliding-window CMN of n_utt feature matrices [frames][f] concatenated in
  * d_in (frame offsets d_frame_off[n_utt + 1]); bit-identical to
  * vox_sliding_cmn per utterance.  Replaces `apply-cmvn-sliding` (tf_extract.py:63). */
 int vox_sliding_cmn_device(const float* d_in, const int64_t* d_frame_off, int n_utt, int f,
                            int cmn_window, int center, float* d_out, void* stream);
+/* Kaldi CompressedMatrix round trip of n_utt feature matrices [frames][f]
+ * concatenated in d_in (`copy-feats --compress=true`, prepare_data.sh:69,
+ * method kAutomaticMethod: "CM " kSpeechFeature for rows > 8, "CM2"
+ * kTwoByteAuto otherwise).  Writes each utterance's compressed payload (the
+ * bytes after the CM token, vox_cm_blob_bytes(rows, f) of them) at
+ * d_blob + d_blob_off[u] (device int64[n_utt]) and, when d_out is non-NULL, the
+ * decoded features as Kaldi's CopyToMat yields them (the matrix
+ * apply-cmvn-sliding reads).  Asynchronous on `stream`.  n_utt <= 65535. */
+int64_t vox_cm_blob_bytes(int rows, int cols);
+int vox_cm_compress_device(const float* d_in, const int64_t* d_frame_off, int n_utt, int f,
+                           uint8_t* d_blob, const int64_t* d_blob_off, float* d_out, void* stream);
 
 const char* vox_last_error(void);
 

@@ -76,6 +76,28 @@ int main(int argc, char** argv) {
       (void)walk(m, &cs, it & 1);
     }
   }
+  // forged dimensions in every header field of the first matrix of each file
+  for (int a = 1; a < argc; ++a) {
+    const std::vector<uint8_t> b = slurp(argv[a]);
+    size_t sp = 0;
+    while (sp < b.size() && b[sp] != ' ') ++sp;
+    for (size_t at = sp + 1; at + 4 <= b.size() && at < sp + 24; ++at) {
+      for (int32_t v : {-1, -7, (int32_t)0x80000000, 0x7fffffff, 0x40000000, 0}) {
+        std::vector<uint8_t> m = b;
+        std::memcpy(&m[at], &v, 4);
+        int rows = 0, cols = 0;
+        const uint8_t* q = m.data() + sp + 1;
+        const size_t nb = m.size() - sp - 1;
+        if (vox_parse_mat_shape(q, nb, &rows, &cols) != VOX_OK) continue;
+        if (rows < 0 || cols < 0) return 4;   // a negative shape must never be accepted
+        if ((int64_t)rows * cols > (int64_t)1 << 26) continue;
+        std::vector<float> o((size_t)rows * cols + 1);
+        size_t used = 0;
+        (void)vox_parse_mat(q, nb, o.data(), rows, cols, &used);
+        (void)vox_parse_mat_kaldi(q, nb, o.data(), rows, cols, &used);
+      }
+    }
+  }
   // file-path readers at every offset of each file (and one past the end)
   for (int a = 1; a < argc; ++a) {
     const std::vector<uint8_t> b = slurp(argv[a]);

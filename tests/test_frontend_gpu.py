@@ -65,6 +65,23 @@ def test_fbank_dither_deterministic():
     assert np.abs(a - d).max() < 0.05               # unit-variance noise on ~2000-amplitude audio
 
 
+def test_fbank_dither_keyed_per_utterance():
+    """Keyed dither: the same waveform under two utterance ids draws different
+    noise, and an id gives the same features at any batch position."""
+    from voxsrc2020_speaker_verification_amd import frontend
+    w = _waves(np.random.default_rng(2), [8000])
+    o = frontend.FbankOptions(dither=1.0, seed=7)
+    a, b = frontend.fbank(w + w, o, keys=["spk1-utt1", "spk1-utt2"])
+    c = frontend.fbank(w + w, o, keys=["x", "spk1-utt2"])[1]
+    d = frontend.fbank(w, o, keys=["spk1-utt1"])[0]
+    assert not np.array_equal(a, b)
+    assert np.array_equal(b, c) and np.array_equal(a, d)
+    e = frontend.fbank(w, o)[0]                     # unkeyed: noise from (seed, frame, sample)
+    assert not np.array_equal(a, e)
+    z = frontend.fbank(w, frontend.FbankOptions(dither=0.0), keys=["spk1-utt1"])[0]
+    assert np.abs(a - z).max() < 0.05
+
+
 @pytest.mark.parametrize("T", [1, 50, 300, 301, 1000, 2345])
 def test_cmn_device_bit_exact(T):
     import torch
@@ -135,3 +152,67 @@ def test_fbank_cli(tmp_path):
         assert np.array_equal(got[f"utt{i}"], exp[i])
     items = list(kaldi.iter_features(scp, cmn=False))
     assert [k for k, _ in items] == ["utt0", "utt1"]
+
+
+def _cm_mats():
+    rng = np.random.default_rng(11)
+    mats = [(rng.standard_normal((T, 80)) * 4 + rng.standard_normal(80) * 6).astype(np.float32)
+            for T in (300, 9, 8, 1, 1234)]
+    q = np.round(rng.standard_normal((57, 80)) * 2).astype(np.float32)   # ties
+    q[:, 3] = 1.5                                                         # constant column
+    mats.append(q)
+    mats.append(np.full((20, 80), -2.25, np.float32))                     # constant matrix
+    mats.append(np.zeros((0, 80), np.float32))                            # empty utterance
+    return mats
+
+
+def test_cm_compress_device_matches_oracle():
+    """vox_cm_compress_device == the CompressedMatrix restatement
+    (oracle/kaldi_ref.cm_encode_kaldi) byte for byte, and its decoded output ==
+    the Kaldi-order host decode of those bytes, bitwise."""
+    import torch
+    from oracle import kaldi_ref
+    from voxsrc2020_speaker_verification_amd import frontend, kaldi
+    mats = _cm_mats()
+    fo = np.zeros(len(mats) + 1, np.int64)
+    fo[1:] = np.cumsum([m.shape[0] for m in mats])
+    feats = torch.from_numpy(np.concatenate(mats)).cuda()
+    out, blob, boff = frontend.cm_compress_device(feats, fo)
+    out, blob = out.cpu().numpy(), blob.cpu().numpy()
+    for i, m in enumerate(mats):
+        pl = blob[boff[i]:boff[i + 1]].tobytes()
+        if m.shape[0] == 0:
+            assert len(pl) == 16
+            continue
+        tok, ref = kaldi_ref.cm_encode_kaldi(m)
+        assert pl == ref, i
+        dec, _ = kaldi.parse_mat(b"\0B" + tok + pl, cm="kaldi")
+        assert np.array_equal(out[fo[i]:fo[i + 1]], dec), i
+
+
+def test_fbank_cli_compress(tmp_path):
+    """--compress true writes Kaldi CM records: the ark decodes (Kaldi order) to
+    what cm_compress_device's round trip gives for the same features."""
+    import torch
+    from voxsrc2020_speaker_verification_amd import frontend, kaldi
+    rng = np.random.default_rng(4)
+    waves = _waves(rng, [5000, 16000, 560])
+    lines = []
+    for i, w in enumerate(waves):
+        p = str(tmp_path / f"u{i}.wav")
+        frontend.write_wav(p, w)
+        lines.append(f"utt{i} {p}")
+    (tmp_path / "wav.scp").write_text("\n".join(lines) + "\n")
+    ark, scp = str(tmp_path / "c.ark"), str(tmp_path / "c.scp")
+    assert frontend.main(["--dither", "0", "--compress", "true", f"scp:{tmp_path}/wav.scp",
+                          f"ark,scp:{ark},{scp}"]) == 0
+    got = dict(kaldi.read_mat_ark(ark, cm="kaldi"))
+    o = frontend.FbankOptions(dither=0.0)
+    feats, fo = frontend.fbank_device(waves, o)
+    rt, _, _ = frontend.cm_compress_device(feats, fo)
+    rt = rt.cpu().numpy()
+    for i in range(3):
+        assert np.array_equal(got[f"utt{i}"], rt[fo[i]:fo[i + 1]])
+    assert got["utt2"].shape[0] == 2            # <= 8 frames: CM2
+    items = dict(kaldi.iter_features(scp, cmn=False))
+    assert np.array_equal(items["utt1"], got["utt1"])

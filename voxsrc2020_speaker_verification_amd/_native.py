@@ -83,6 +83,11 @@ _SIGS = [
     ("vox_fbank_num_frames", C.c_int64, [C.c_int64, _FO]),
     ("vox_fbank_device", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int64, _FO,
                                    C.c_void_p, C.c_void_p]),
+    ("vox_fbank_device_keyed", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
+                                         C.c_int64, _FO, C.c_void_p, C.c_void_p]),
+    ("vox_cm_blob_bytes", C.c_int64, [C.c_int, C.c_int]),
+    ("vox_cm_compress_device", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p,
+                                         C.c_void_p, C.c_void_p, C.c_void_p]),
     ("vox_sliding_cmn_device", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int,
                                          C.c_int, C.c_void_p, C.c_void_p]),
     ("vox_format_vec_flt", C.c_int64, [C.c_char_p, _F, C.c_int, C.c_void_p, C.c_size_t,

@@ -27,6 +27,7 @@
 #include <limits>
 #include <mutex>
 #include <string>
+#include <deque>
 #include <vector>
 
 #include "../../include/voxemb.h"
@@ -65,7 +66,8 @@ __device__ __forceinline__ float gauss(unsigned long long key) {
 template <int NFFT>
 __global__ __launch_bounds__(64) void fbank_k(const float* __restrict__ wav,
                                               const int64_t* __restrict__ samp_off,
-                                              const int64_t* __restrict__ frame_off, int n_utt,
+                                              const int64_t* __restrict__ frame_off,
+                                              const uint64_t* __restrict__ utt_key, int n_utt,
                                               FbankDev d, float* __restrict__ out) {
   constexpr int NC = NFFT / 2;          // complex FFT size
   constexpr int LOGNC = NC == 256 ? 8 : 7;
@@ -85,6 +87,9 @@ __global__ __launch_bounds__(64) void fbank_k(const float* __restrict__ wav,
   const int64_t t = f - frame_off[u];
   const float* src = wav + samp_off[u] + t * d.frame_shift;
   const int L = d.frame_len;
+  // per-utterance stream: the caller's key (a hash of the utterance id) keeps the
+  // noise independent across utterances yet the same at any batch position
+  const unsigned long long dkey = d.seed ^ (utt_key ? mix64(utt_key[u] ^ 0xD1B54A32D192ED03ull) : 0ull);
 
   // 1. extract (+ dither), 2. DC offset
   float v[(NFFT + 63) / 64];
@@ -96,7 +101,7 @@ __global__ __launch_bounds__(64) void fbank_k(const float* __restrict__ wav,
     if (i < L) {
       x = src[i];
       if (d.dither != 0.f)
-        x += d.dither * gauss(d.seed ^ mix64(((unsigned long long)t << 16) ^ (unsigned)i));
+        x += d.dither * gauss(dkey ^ mix64(((unsigned long long)t << 16) ^ (unsigned)i));
     }
     v[k] = x;
     part += x;
@@ -226,6 +231,180 @@ __global__ void cmn_k(const float* __restrict__ in, const int64_t* __restrict__ 
   }
 }
 
+// ---- Kaldi CompressedMatrix round trip (`copy-feats --compress=true`,
+// prepare_data.sh:69; Kaldi compressed-matrix.cc, not vendored: its published
+// kAutomaticMethod -> kSpeechFeature for rows > 8, kTwoByteAuto otherwise).
+// Per utterance the blob is what follows the "CM " / "CM2" token:
+//   float min, float range, int32 rows, int32 cols,
+//   rows > 8:  uint16 [cols][4] percentiles (0, 25, 75, 100), uint8 [cols][rows]
+//   rows <= 8: uint16 [rows][cols]
+// cm_head_k writes the global header; cm_col_k one column: the four order
+// statistics by a 4 x 8-bit radix select (exact, as Kaldi's nth_element
+// chain), the column header, the bytes, and the decoded values in Kaldi C++
+// CopyToMat order (the one apply-cmvn-sliding sees, tf_extract.py:63).
+__device__ __forceinline__ unsigned cm_key(float v) {
+  const unsigned u = __float_as_uint(v);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float cm_unkey(unsigned k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+// FloatToUint16: float ratio, clamp, + 0.499 in double, truncate
+__device__ __forceinline__ int cm_u16(float mn, float range, float v) {
+  float f = (v - mn) / range;
+  if (f > 1.0f) f = 1.0f;
+  if (f < 0.0f) f = 0.0f;
+  return (int)((double)(f * 65535.0f) + 0.499);
+}
+// Uint16ToFloat: min + range * 1.52590218966964e-05f * v, float, left to right
+__device__ __forceinline__ float cm_f16(float mn, float range, int v) {
+  return mn + (range * 1.52590218966964e-05f) * (float)v;
+}
+__device__ __forceinline__ int cm_char(float p0, float p25, float p75, float p100, float v) {
+  int a;
+  if (v < p25) {
+    const float f = (v - p0) / (p25 - p0);
+    a = (int)((double)(f * 64.0f) + 0.5);
+    a = a < 0 ? 0 : (a > 64 ? 64 : a);
+  } else if (v < p75) {
+    const float f = (v - p25) / (p75 - p25);
+    a = 64 + (int)((double)(f * 128.0f) + 0.5);
+    a = a < 64 ? 64 : (a > 192 ? 192 : a);
+  } else {
+    const float f = (v - p75) / (p100 - p75);
+    a = 192 + (int)((double)(f * 63.0f) + 0.5);
+    a = a < 192 ? 192 : (a > 255 ? 255 : a);
+  }
+  return a;
+}
+__device__ __forceinline__ float cm_unchar(float p0, float p25, float p75, float p100, int v) {
+  double x;
+  if (v <= 64) x = (double)p0 + (double)((p25 - p0) * (float)v) * (1 / 64.0);
+  else if (v <= 192) x = (double)p25 + (double)((p75 - p25) * (float)(v - 64)) * (1 / 128.0);
+  else x = (double)p75 + (double)((p100 - p75) * (float)(v - 192)) * (1 / 63.0);
+  return (float)x;
+}
+
+__global__ __launch_bounds__(256) void cm_head_k(const float* __restrict__ in,
+                                                 const int64_t* __restrict__ frame_off, int F,
+                                                 uint8_t* __restrict__ blob,
+                                                 const int64_t* __restrict__ blob_off) {
+  const int u = blockIdx.x;
+  const int64_t base = frame_off[u];
+  const int T = (int)(frame_off[u + 1] - base);
+  const float* x = in + base * F;
+  float mn = INFINITY, mx = -INFINITY;
+  for (long i = threadIdx.x; i < (long)T * F; i += 256) {
+    const float v = x[i];
+    mn = fminf(mn, v);
+    mx = fmaxf(mx, v);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    mn = fminf(mn, __shfl_xor(mn, o, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  }
+  __shared__ float smn[4], smx[4];
+  if ((threadIdx.x & 63) == 0) {
+    smn[threadIdx.x >> 6] = mn;
+    smx[threadIdx.x >> 6] = mx;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    mn = fminf(fminf(smn[0], smn[1]), fminf(smn[2], smn[3]));
+    mx = fmaxf(fmaxf(smx[0], smx[1]), fmaxf(smx[2], smx[3]));
+    if (T == 0) mn = mx = 0.f;
+    // ComputeGlobalHeader: a constant matrix gets max = min + (1 + |min|)
+    if (mx == mn) mx = (float)((double)mn + (1.0 + fabs((double)mn)));
+    const float hdr[2] = {mn, mx - mn};
+    const int dims[2] = {T, F};
+    uint8_t* b = blob + blob_off[u];
+    __builtin_memcpy(b, hdr, 8);
+    __builtin_memcpy(b + 8, dims, 8);
+  }
+}
+
+__global__ __launch_bounds__(256) void cm_col_k(const float* __restrict__ in,
+                                                const int64_t* __restrict__ frame_off, int F,
+                                                uint8_t* __restrict__ blob,
+                                                const int64_t* __restrict__ blob_off,
+                                                float* __restrict__ out) {
+  const int c = blockIdx.x, u = blockIdx.y, tid = threadIdx.x;
+  const int64_t base = frame_off[u];
+  const int T = (int)(frame_off[u + 1] - base);
+  if (T == 0) return;
+  const float* x = in + base * F + c;
+  uint8_t* b = blob + blob_off[u];
+  float hdr[2];
+  __builtin_memcpy(hdr, b, 8);
+  const float mn = hdr[0], range = hdr[1];
+  if (T <= 8) {   // kTwoByteAuto ("CM2"): uint16 row-major, min + v * (range / 65535)
+    const float inc = (float)((double)range * (1.0 / 65535.0));
+    for (int t = tid; t < T; t += 256) {
+      const int q = cm_u16(mn, range, x[(long)t * F]);
+      const uint16_t q16 = (uint16_t)q;
+      __builtin_memcpy(b + 16 + 2 * ((long)t * F + c), &q16, 2);
+      if (out) out[(base + t) * F + c] = mn + (float)q16 * inc;
+    }
+    return;
+  }
+  __shared__ unsigned hist[4][256];
+  __shared__ unsigned pref[4];
+  __shared__ int want[4];
+  __shared__ float pf[4];
+  const int qr = T / 4;
+  if (tid < 4) {
+    pref[tid] = 0;
+    want[tid] = tid == 0 ? 0 : tid == 1 ? qr : tid == 2 ? 3 * qr : T - 1;
+  }
+  for (int pass = 0; pass < 4; ++pass) {
+    const int shift = 24 - 8 * pass;
+    const unsigned hi = pass == 0 ? 0u : (0xFFFFFFFFu << (32 - 8 * pass));
+    for (int i = tid; i < 4 * 256; i += 256) (&hist[0][0])[i] = 0;
+    __syncthreads();
+    for (int t = tid; t < T; t += 256) {
+      const unsigned k = cm_key(x[(long)t * F]);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if ((k & hi) == pref[r]) atomicAdd(&hist[r][(k >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    if (tid < 4) {
+      unsigned cum = 0;
+      int d = 0;
+      for (; d < 255; ++d) {
+        if (cum + hist[tid][d] > (unsigned)want[tid]) break;
+        cum += hist[tid][d];
+      }
+      want[tid] -= (int)cum;
+      pref[tid] |= (unsigned)d << shift;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    // ComputeColHeader (rows >= 5): strictly increasing uint16 percentiles
+    int p[4];
+    p[0] = min(cm_u16(mn, range, cm_unkey(pref[0])), 65532);
+    p[1] = min(max(cm_u16(mn, range, cm_unkey(pref[1])), p[0] + 1), 65533);
+    p[2] = min(max(cm_u16(mn, range, cm_unkey(pref[2])), p[1] + 1), 65534);
+    p[3] = max(cm_u16(mn, range, cm_unkey(pref[3])), p[2] + 1);
+    uint16_t h16[4];
+    for (int r = 0; r < 4; ++r) {
+      h16[r] = (uint16_t)p[r];
+      pf[r] = cm_f16(mn, range, h16[r]);
+    }
+    __builtin_memcpy(b + 16 + 8 * c, h16, 8);
+  }
+  __syncthreads();
+  const float p0 = pf[0], p25 = pf[1], p75 = pf[2], p100 = pf[3];
+  uint8_t* col = b + 16 + 8 * (long)F + (long)c * T;
+  for (int t = tid; t < T; t += 256) {
+    const int a = cm_char(p0, p25, p75, p100, x[(long)t * F]);
+    col[t] = (uint8_t)a;
+    if (out) out[(base + t) * F + c] = cm_unchar(p0, p25, p75, p100, a);
+  }
+}
+
 namespace {
 // MelBanks (mel-computations.cc) in float32, Kaldi's operation order
 inline float mel_scale(float f) { return 1127.0f * logf(1.0f + f / 700.0f); }
@@ -243,7 +422,7 @@ struct FbankTables {
   }
 };
 std::mutex g_tab_mu;
-std::vector<FbankTables> g_tabs;   // one per (device, shape)
+std::deque<FbankTables> g_tabs;   // one per (device, shape); deque: push_back keeps references valid
 
 template <typename T>
 hipError_t upload(T** dst, const std::vector<T>& v) {
@@ -366,9 +545,10 @@ extern "C" int64_t vox_fbank_num_frames(int64_t num_samples, const vox_fbank_opt
   return 1 + (num_samples - L) / S;
 }
 
-extern "C" int vox_fbank_device(const float* d_wav, const int64_t* d_samp_off,
-                                const int64_t* d_frame_off, int n_utt, int64_t total_frames,
-                                const vox_fbank_opts* o, float* d_out, void* stream) {
+extern "C" int vox_fbank_device_keyed(const float* d_wav, const int64_t* d_samp_off,
+                                      const int64_t* d_frame_off, const uint64_t* d_utt_key,
+                                      int n_utt, int64_t total_frames, const vox_fbank_opts* o,
+                                      float* d_out, void* stream) {
   if (!d_wav || !d_samp_off || !d_frame_off || !d_out || n_utt <= 0 || total_frames < 0)
     return vox_set_error(VOX_EINVAL, "bad fbank arguments");
   int L, S, nfft;
@@ -391,15 +571,22 @@ extern "C" int vox_fbank_device(const float* d_wav, const int64_t* d_samp_off,
     hipStream_t s = (hipStream_t)stream;
     if (nfft == 512)
       hipLaunchKernelGGL(fbank_k<512>, dim3((unsigned)total_frames), dim3(64), 0, s, d_wav,
-                         d_samp_off, d_frame_off, n_utt, d, d_out);
+                         d_samp_off, d_frame_off, d_utt_key, n_utt, d, d_out);
     else
       hipLaunchKernelGGL(fbank_k<256>, dim3((unsigned)total_frames), dim3(64), 0, s, d_wav,
-                         d_samp_off, d_frame_off, n_utt, d, d_out);
+                         d_samp_off, d_frame_off, d_utt_key, n_utt, d, d_out);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) rc = vox_set_error(VOX_EHIP, (std::string("fbank_k: ") + hipGetErrorString(e)).c_str());
   }
   (void)hipSetDevice(prev);
   return rc;
+}
+
+extern "C" int vox_fbank_device(const float* d_wav, const int64_t* d_samp_off,
+                                const int64_t* d_frame_off, int n_utt, int64_t total_frames,
+                                const vox_fbank_opts* o, float* d_out, void* stream) {
+  return vox_fbank_device_keyed(d_wav, d_samp_off, d_frame_off, nullptr, n_utt, total_frames, o,
+                                d_out, stream);
 }
 
 extern "C" int vox_sliding_cmn_device(const float* d_in, const int64_t* d_frame_off, int n_utt,
@@ -419,5 +606,34 @@ extern "C" int vox_sliding_cmn_device(const float* d_in, const int64_t* d_frame_
   hipError_t e = hipGetLastError();
   (void)hipSetDevice(prev);
   if (e != hipSuccess) return vox_set_error(VOX_EHIP, (std::string("cmn_k: ") + hipGetErrorString(e)).c_str());
+  return VOX_OK;
+}
+
+extern "C" int64_t vox_cm_blob_bytes(int rows, int cols) {
+  if (rows < 0 || cols <= 0) return vox_set_error(VOX_EINVAL, "cm: bad matrix shape");
+  if (rows > 8) return 16 + 8 * (int64_t)cols + (int64_t)rows * cols;
+  return 16 + 2 * (int64_t)rows * cols;
+}
+
+extern "C" int vox_cm_compress_device(const float* d_in, const int64_t* d_frame_off, int n_utt,
+                                      int f, uint8_t* d_blob, const int64_t* d_blob_off,
+                                      float* d_out, void* stream) {
+  if (!d_in || !d_frame_off || !d_blob || !d_blob_off || n_utt <= 0 || f <= 0 || n_utt > 65535)
+    return vox_set_error(VOX_EINVAL, "bad cm arguments");
+  hipPointerAttribute_t at;
+  if (hipPointerGetAttributes(&at, d_in) != hipSuccess || at.type != hipMemoryTypeDevice)
+    return vox_set_error(VOX_EINVAL, "cm: features must be device memory");
+  int prev = -1;
+  if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(at.device) != hipSuccess)
+    return vox_set_error(VOX_EHIP, "cm: cannot select the features' device");
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(cm_head_k, dim3(n_utt), dim3(256), 0, s, d_in, d_frame_off, f, d_blob,
+                     d_blob_off);
+  hipLaunchKernelGGL(cm_col_k, dim3(f, n_utt), dim3(256), 0, s, d_in, d_frame_off, f, d_blob,
+                     d_blob_off, d_out);
+  hipError_t e = hipGetLastError();
+  (void)hipSetDevice(prev);
+  if (e != hipSuccess)
+    return vox_set_error(VOX_EHIP, (std::string("cm kernels: ") + hipGetErrorString(e)).c_str());
   return VOX_OK;
 }

@@ -73,7 +73,8 @@ struct Reader {
   const uint8_t* p;
   size_t n, i = 0;
   bool take(void* dst, size_t k) {
-    if (i + k > n) return false;
+    if (k > n - i) return false;   // i <= n always; no wraparound for huge k
+    if (k == 0) return true;       // dst may be null for an empty matrix
     std::memcpy(dst, p + i, k);
     i += k;
     return true;
@@ -81,21 +82,22 @@ struct Reader {
 };
 
 // Parse the header; on success sets rows/cols/kind and leaves r at the payload.
-int parse_header(Reader& r, int* rows, int* cols, int* kind /*0 FM 1 DM 2 CM*/) {
+int parse_header(Reader& r, int* rows, int* cols, int* kind /*0 FM 1 DM 2 CM 3 CM2*/) {
   char b[2];
   if (!r.take(b, 2)) return kfail(VOX_EIO, "truncated matrix");
   if (b[0] != '\0' || b[1] != 'B') return kfail(VOX_EIO, "not a binary Kaldi matrix (ascii unsupported)");
   char h[3];
   if (!r.take(h, 3)) return kfail(VOX_EIO, "truncated matrix header");
   if (h[0] == 'C' && h[1] == 'M') {
-    if (h[2] != ' ') return kfail(VOX_EIO, "CM2/CM3 compressed formats are not supported");
+    if (h[2] != ' ' && h[2] != '2') return kfail(VOX_EIO, "CM3 compressed format is not supported");
     float mn, range;
     int32_t nr, nc;
     if (!r.take(&mn, 4) || !r.take(&range, 4) || !r.take(&nr, 4) || !r.take(&nc, 4))
       return kfail(VOX_EIO, "truncated CM header");
+    if (nr < 0 || nc < 0) return kfail(VOX_EIO, "negative matrix dims");
     *rows = nr;
     *cols = nc;
-    *kind = 2;
+    *kind = h[2] == '2' ? 3 : 2;
     return VOX_OK;
   }
   if (h[0] == 'F' && h[1] == 'M' && h[2] == ' ') *kind = 0;
@@ -129,10 +131,20 @@ int parse_payload(Reader& r, int kind, int rows, int cols, float* out, int cm_ka
     for (size_t i = 0; i < n; ++i) out[i] = (float)d[i];
     return VOX_OK;
   }
-  // CM: re-read the global header fields that precede the column headers
+  // CM / CM2: re-read the global header fields that precede the payload
   float mn, range;
   std::memcpy(&mn, r.p + r.i - 16, 4);
   std::memcpy(&range, r.p + r.i - 12, 4);
+  if (kind == 3) {
+    // CM2 (kTwoByte, Kaldi CopyToMat): min + v * float(range * (1 / 65535.0)),
+    // uint16 row-major; kaldi_io has no CM2 reader (kaldi_io.py:477 asserts "CM ")
+    if (!cm_kaldi) return kfail(VOX_EIO, "CM2 is not readable by kaldi_io (use cm=\"kaldi\")");
+    std::vector<uint16_t> q(n);
+    if (!r.take(q.data(), n * 2)) return kfail(VOX_EIO, "truncated CM2 payload");
+    const float inc = (float)((double)range * (1.0 / 65535.0));
+    for (size_t i = 0; i < n; ++i) out[i] = mn + (float)q[i] * inc;
+    return VOX_OK;
+  }
   std::vector<uint16_t> ch((size_t)cols * 4);
   if (!r.take(ch.data(), ch.size() * 2)) return kfail(VOX_EIO, "truncated CM column headers");
   std::vector<uint8_t> data(n);
@@ -151,7 +163,7 @@ int parse_payload(Reader& r, int kind, int rows, int cols, float* out, int cm_ka
         p[k] = v + mn;
       }
     }
-    const uint8_t* d = &data[(size_t)col * rows];  // column-major
+    const uint8_t* d = data.data() + (size_t)col * rows;  // column-major
     if (cm_kaldi) {
       for (int row = 0; row < rows; ++row) {
         const unsigned v = d[row];
@@ -208,6 +220,7 @@ int read_file_at(const char* path, int64_t offset, std::vector<uint8_t>& buf) {
   size_t total = r.i;
   if (kind == 0) total += (size_t)rows * cols * 4;
   else if (kind == 1) total += (size_t)rows * cols * 8;
+  else if (kind == 3) total += (size_t)rows * cols * 2;
   else total += (size_t)cols * 8 + (size_t)rows * cols;
   if ((size_t)offset + total > (size_t)size) {
     std::fclose(f);

@@ -10,14 +10,20 @@ Reference steps replaced:
     `kaldi.sliding_cmn`);
   * `tf_extract.py` on those features -> `embed_wavs` (chunk rule and
     batching of `extract.embed_utterances`, features never leave HBM).
-Not reproduced: `copy-feats --compress` (prepare_data.sh:69) between the two
-Kaldi steps -- a lossy 8-bit codec the on-device path has no reason to apply
-(`kaldi.read_mat(..., cm="kaldi")` decodes such arks exactly as Kaldi does).
+  * `copy-feats --compress=true` (prepare_data.sh:69) between the two Kaldi
+    steps -> `cm_compress_device` (Kaldi CompressedMatrix, kAutomaticMethod):
+    the lossy 8-bit codec the reference's features pass through.  Opt-in
+    (`embed_wavs(compress=True)`, CLI `--compress`), so reference-parity runs
+    see the same quantised features; `kaldi.read_mat(..., cm="kaldi")`
+    decodes the written arks exactly as Kaldi does.
 Kaldi's default dither (1.0, random) is supported with a counter-based
-generator; dither=0 gives deterministic features (used by the parity tests).
+generator keyed by (seed, utterance key, frame, sample): each utterance draws
+its own noise, as Kaldi's per-utterance RandomState does, and the result does
+not depend on batch composition; dither=0 gives deterministic features (used by
+the parity tests).
 
-Kernels: libvoxemb `vox_fbank_device` / `vox_sliding_cmn_device`
-(csrc/fbank.hip).  No CPU fallback.
+Kernels: libvoxemb `vox_fbank_device_keyed` / `vox_cm_compress_device` /
+`vox_sliding_cmn_device` (csrc/fbank.hip).  No CPU fallback.
 
     python -m voxsrc2020_speaker_verification_amd.frontend \\
         --config conf/fbank80.conf scp:data/voxceleb1/wav.scp \\
@@ -28,6 +34,7 @@ from __future__ import annotations
 
 import argparse
 import ctypes as C
+import hashlib
 import os
 import struct
 import sys
@@ -143,14 +150,20 @@ def read_wav_scp(path):
 
 
 # ------------------------------------------------------------------ device ops
+def utt_dither_key(key):
+    """64-bit dither key of an utterance id (stable across runs and hosts)."""
+    return int.from_bytes(hashlib.blake2b(str(key).encode(), digest_size=8).digest(), "little")
+
+
 def _dev(device):
     import torch
     return torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
 
 
-def fbank_device(waves, opts=None, device=0, stream=None):
-    """waves: list of 1-D float arrays/tensors.  Returns (feats [sum T, bins]
-    float32 on the device, frame offsets int64 [n+1] host, sample offsets)."""
+def fbank_device(waves, opts=None, device=0, stream=None, keys=None):
+    """waves: list of 1-D float arrays/tensors; keys: optional utterance ids
+    (one per wave) that key the dither noise per utterance.  Returns (feats
+    [sum T, bins] float32 on the device, frame offsets int64 [n+1] host)."""
     import torch
     opts = opts or FbankOptions()
     dev = _dev(device)
@@ -167,13 +180,22 @@ def fbank_device(waves, opts=None, device=0, stream=None):
             flat[int(a):int(a) + t.shape[0]] = t.to(dev, torch.float32)
         so = torch.from_numpy(samp_off).to(dev)
         fo = torch.from_numpy(frame_off).to(dev)
+        uk = None
+        if keys is not None:
+            if len(keys) != len(waves):
+                raise ValueError(f"{len(keys)} keys for {len(waves)} waveforms")
+            kv = np.array([utt_dither_key(k) for k in keys], np.uint64).view(np.int64)
+            uk = torch.from_numpy(kv).to(dev)
         out = torch.empty((int(frame_off[-1]), opts.num_mel_bins), dtype=torch.float32, device=dev)
         s = stream or torch.cuda.current_stream(dev)
+        # the uploads above ran on the current stream: order the kernel after them
+        s.wait_stream(torch.cuda.current_stream(dev))
         if len(waves):
-            check(lib().vox_fbank_device(C.c_void_p(flat.data_ptr()), C.c_void_p(so.data_ptr()),
-                                         C.c_void_p(fo.data_ptr()), len(waves), int(frame_off[-1]),
-                                         C.byref(opts.c()), C.c_void_p(out.data_ptr()),
-                                         C.c_void_p(s.cuda_stream)))
+            check(lib().vox_fbank_device_keyed(
+                C.c_void_p(flat.data_ptr()), C.c_void_p(so.data_ptr()), C.c_void_p(fo.data_ptr()),
+                C.c_void_p(uk.data_ptr() if uk is not None else None), len(waves),
+                int(frame_off[-1]), C.byref(opts.c()), C.c_void_p(out.data_ptr()),
+                C.c_void_p(s.cuda_stream)))
         s.synchronize()   # the offsets / waveform tensors die with this frame
     return out, frame_off
 
@@ -190,6 +212,7 @@ def sliding_cmn_device(feats, frame_off, cmn_window=300, center=True, stream=Non
     with torch.cuda.device(dev):
         fo = torch.from_numpy(np.asarray(frame_off, np.int64)).to(dev)
         s = stream or torch.cuda.current_stream(dev)
+        s.wait_stream(torch.cuda.current_stream(dev))   # fo and feats were produced there
         check(lib().vox_sliding_cmn_device(C.c_void_p(feats.data_ptr()), C.c_void_p(fo.data_ptr()),
                                            n, feats.shape[1], int(cmn_window), 1 if center else 0,
                                            C.c_void_p(out.data_ptr()), C.c_void_p(s.cuda_stream)))
@@ -197,22 +220,73 @@ def sliding_cmn_device(feats, frame_off, cmn_window=300, center=True, stream=Non
     return out
 
 
-def fbank(waves, opts=None, device=0, cmn=False):
+def cm_blob_bytes(rows, cols):
+    """Bytes of a compressed payload after its "CM " (rows > 8) / "CM2" token."""
+    return check(lib().vox_cm_blob_bytes(int(rows), int(cols)))
+
+
+def cm_compress_device(feats, frame_off, stream=None, decode=True):
+    """`copy-feats --compress=true` over every utterance of a concatenated
+    device feature matrix: returns (decoded features [sum T, F] float32 on the
+    device as Kaldi's CopyToMat yields them, or None; uint8 device blob; int64
+    host blob offsets [n+1]).  Utterance u's payload is
+    blob[off[u]:off[u+1]], to follow b"CM " if it has > 8 frames else b"CM2"."""
+    import torch
+    dev = feats.device
+    fo = np.asarray(frame_off, np.int64)
+    n, F = len(fo) - 1, int(feats.shape[1])
+    sizes = [cm_blob_bytes(int(fo[i + 1] - fo[i]), F) for i in range(n)]
+    boff = np.zeros(n + 1, np.int64)
+    boff[1:] = np.cumsum(sizes)
+    blob = torch.empty(int(boff[-1]), dtype=torch.uint8, device=dev)
+    out = torch.empty_like(feats) if decode else None
+    if n <= 0:
+        return out, blob, boff
+    with torch.cuda.device(dev):
+        fo_d = torch.from_numpy(fo).to(dev)
+        bo_d = torch.from_numpy(boff[:-1].copy()).to(dev)
+        s = stream or torch.cuda.current_stream(dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        for lo in range(0, n, 65535):    # grid.y limit
+            hi = min(n, lo + 65535)
+            check(lib().vox_cm_compress_device(
+                C.c_void_p(feats.data_ptr()), C.c_void_p(fo_d[lo:].data_ptr()), hi - lo, F,
+                C.c_void_p(blob.data_ptr()), C.c_void_p(bo_d[lo:].data_ptr()),
+                C.c_void_p(out.data_ptr() if out is not None else None),
+                C.c_void_p(s.cuda_stream)))
+        s.synchronize()
+    return out, blob, boff
+
+
+def format_cm_record(key, payload, rows):
+    """Bytes of one compressed ark record and the offset of its '\\0B'."""
+    k = key.encode("utf-8")
+    if not k or b" " in k:
+        raise ValueError("key must be non-empty without spaces")
+    return k + b" \0B" + (b"CM " if rows > 8 else b"CM2") + bytes(payload), len(k) + 1
+
+
+def fbank(waves, opts=None, device=0, cmn=False, keys=None):
     """Host convenience: list of waveforms -> list of [T, bins] numpy arrays."""
-    feats, fo = fbank_device(waves, opts, device)
+    feats, fo = fbank_device(waves, opts, device, keys=keys)
     if cmn:
         feats = sliding_cmn_device(feats, fo)
     h = feats.cpu().numpy()
     return [h[fo[i]:fo[i + 1]] for i in range(len(waves))]
 
 
-def embed_wavs(extractor, waves, opts=None, batch=64, cmn=True):
-    """wav -> embeddings with features resident on the device: fbank, CMN,
-    the tf_extract chunk rule (<= 1000-frame chunks, length-weighted mean) with
-    equal-length chunks batched (extract.embed_utterances)."""
+def embed_wavs(extractor, waves, opts=None, batch=64, cmn=True, keys=None, compress=False):
+    """wav -> embeddings with features resident on the device: fbank,
+    [CM round trip,] CMN, the tf_extract chunk rule (<= 1000-frame chunks,
+    length-weighted mean) with equal-length chunks batched
+    (extract.embed_utterances).  keys: utterance ids for the per-utterance
+    dither stream; compress: apply the reference's `copy-feats --compress`
+    quantisation (prepare_data.sh:69) before CMN."""
     import torch
     from .extract import embed_utterances
-    feats, fo = fbank_device(waves, opts, extractor.device)
+    feats, fo = fbank_device(waves, opts, extractor.device, keys=keys)
+    if compress:
+        feats, _, _ = cm_compress_device(feats, fo)
     if cmn:
         feats = sliding_cmn_device(feats, fo)
     dev = feats.device
@@ -243,6 +317,8 @@ def main(argv=None):
     ap.add_argument("--dither", type=float, default=None)
     ap.add_argument("--device", type=int, default=0)
     ap.add_argument("--batch", type=int, default=256, help="utterances per device call")
+    ap.add_argument("--compress", default="false", choices=["true", "false"],
+                    help="write Kaldi compressed (CM) matrices, as copy-feats --compress=true")
     ap.add_argument("rspec", help="scp:wav.scp")
     ap.add_argument("wspec", help="ark:feats.ark or ark,scp:feats.ark,feats.scp")
     a = ap.parse_args(argv)
@@ -263,8 +339,17 @@ def main(argv=None):
                 if rate != int(opts.sample_frequency):
                     raise SystemExit(f"{key}: sample rate {rate} != {opts.sample_frequency}")
                 waves.append(w)
-            for (key, _), m in zip(part, fbank(waves, opts, a.device)):
-                rec, off = format_mat_flt(key, m)
+            keys = [k for k, _ in part]
+            if a.compress == "true":
+                feats, fo = fbank_device(waves, opts, a.device, keys=keys)
+                _, blob, boff = cm_compress_device(feats, fo, decode=False)
+                hb = blob.cpu().numpy()
+                recs = [format_cm_record(k, hb[boff[i]:boff[i + 1]], int(fo[i + 1] - fo[i]))
+                        for i, k in enumerate(keys)]
+            else:
+                recs = [format_mat_flt(k, m) for k, m in zip(keys, fbank(waves, opts, a.device,
+                                                                         keys=keys))]
+            for key, (rec, off) in zip(keys, recs):
                 pos = fa.tell()
                 fa.write(rec)
                 fs.write(f"{key} {ark}:{pos + off}\n")
