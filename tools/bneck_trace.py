@@ -8,6 +8,7 @@ import sys
 
 import numpy as np
 
+os.environ.setdefault("VOXEMB_LIB", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "voxsrc2020_speaker_verification_amd", "libvoxemb_diag.so"))
 os.environ["VOXEMB_BNECK_DBG"] = str(256 | int(os.environ.get("VOXEMB_BNECK_DBG", "0")))
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)

@@ -1,5 +1,7 @@
 #!/bin/bash
 # per-op times of the gemm1x1_wide launches under its diagnostic variants
+# diagnostic variants live in the VOX_DIAG build (python -m voxsrc2020_speaker_verification_amd.build_native --diag)
+export VOXEMB_LIB=${VOXEMB_LIB:-$PWD/voxsrc2020_speaker_verification_amd/libvoxemb_diag.so}
 O=gpurun_out/gvar
 mkdir -p $O
 for v in ${VALUES:-0 11 12 14 15 16}; do

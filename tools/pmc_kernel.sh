@@ -1,6 +1,6 @@
 #!/bin/bash
 # SQ counters for the kernels matching $KERNEL (regex), one pass each set,
-# --kernel-trace only; extra env (e.g. VOXEMB_CONV3_WIN=1) passes through.
+# --kernel-trace only; extra env (e.g. VOXEMB_NO_CONV3_RW=1) passes through.
 export TMPDIR=/tmp
 K=${KERNEL:-conv3x3}
 O=gpurun_out/pmck_${TAG:-x}

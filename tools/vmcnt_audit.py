@@ -138,9 +138,13 @@ def audit(ins, max_states=64):
             if VMEM.match(op):
                 operands = insn[len(op):]
                 if "load" in op:
-                    dst = regs(operands.split(",")[0])
-                    src = regs(",".join(operands.split(",")[1:]))
-                    bad = (src | dst) & pend
+                    # global_load_lds: the first operand is the address (the data
+                    # goes to LDS); a load's destination may be the destination
+                    # of an older in-flight load (loads return in order)
+                    lds = "_lds" in op
+                    dst = set() if lds else regs(operands.split(",")[0])
+                    src = regs(operands) if lds else regs(",".join(operands.split(",")[1:]))
+                    bad = src & pend
                     if bad:
                         hits.append((bi, insn, sorted(bad)))
                     q.append(tuple(sorted(dst)))
@@ -212,8 +216,9 @@ def _step(insn, q, hits=None, bi=None):
     if VMEM.match(op):
         operands = insn[len(op):]
         if "load" in op:
-            dst = regs(operands.split(",")[0])
-            bad = used & pend
+            lds = "_lds" in op
+            dst = set() if lds else regs(operands.split(",")[0])
+            bad = (used - dst) & pend
             q.append(tuple(sorted(dst)))
         else:
             bad = used & pend

@@ -10,6 +10,9 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libvoxemb.so")
+# diagnostic build (-DVOX_DIAG: timing variants that skip work, for tools/;
+# load it with VOXEMB_LIB=.../libvoxemb_diag.so)
+DIAG_LIB = os.path.join(HERE, "libvoxemb_diag.so")
 ARCH = os.environ.get("VOX_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = [
@@ -20,7 +23,6 @@ SOURCES = [
     ("gemm_wide.hip", ["-O3"]),
     ("gconv.hip", ["-O3"]),
     ("conv3.hip", ["-O3"]),
-    ("conv3w.hip", ["-O3"]),
     ("conv3r.hip", ["-O3"]),
     ("conv3u.hip", ["-O3"]),
     ("conv3s.hip", ["-O3"]),
@@ -37,15 +39,17 @@ def _hipcc():
     raise RuntimeError("hipcc not found")
 
 
-def build(verbose=False, force=False) -> str:
-    outdir = os.path.join(HERE, "..", "build", "native")
+def build(verbose=False, force=False, diag=False) -> str:
+    outdir = os.path.join(HERE, "..", "build", "native_diag" if diag else "native")
+    lib = DIAG_LIB if diag else LIB
+    dflags = ["-DVOX_DIAG"] if diag else []
     os.makedirs(outdir, exist_ok=True)
     hipcc = _hipcc()
     hdr = os.path.join(HERE, "..", "include", "voxemb.h")
     newest_hdr = max([os.path.getmtime(hdr), os.path.getmtime(__file__)] +
                      [os.path.getmtime(os.path.join(CSRC, n)) for n in os.listdir(CSRC)
                       if n.endswith(".h")])
-    objs, relink, jobs = [], force or not os.path.exists(LIB), []
+    objs, relink, jobs = [], force or not os.path.exists(lib), []
     for src, flags in SOURCES:
         path = os.path.join(CSRC, src)
         obj = os.path.join(outdir, src + ".o")
@@ -55,7 +59,7 @@ def build(verbose=False, force=False) -> str:
             continue
         lang = ["-x", "hip"] if src.endswith(".hip") else []
         jobs.append([hipcc, f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-c", *lang,
-                     path, "-o", obj, *flags])
+                     path, "-o", obj, *flags, *dflags])
     if jobs:
         from concurrent.futures import ThreadPoolExecutor
 
@@ -67,12 +71,12 @@ def build(verbose=False, force=False) -> str:
         with ThreadPoolExecutor(max_workers=min(len(jobs), 6)) as pool:
             list(pool.map(_cc, jobs))
         relink = True
-    if not relink and all(os.path.getmtime(LIB) >= os.path.getmtime(o) for o in objs):
-        return LIB
-    cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs]
+    if not relink and all(os.path.getmtime(lib) >= os.path.getmtime(o) for o in objs):
+        return lib
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib, *objs]
     subprocess.run(cmd, check=True)
-    return LIB
+    return lib
 
 
 if __name__ == "__main__":
-    print(build(verbose=True, force="--force" in sys.argv))
+    print(build(verbose=True, force="--force" in sys.argv, diag="--diag" in sys.argv))

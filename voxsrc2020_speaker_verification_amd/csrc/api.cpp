@@ -236,41 +236,72 @@ struct vox_model {
   hipGraphExec_t graph_exec = nullptr;
   DevBuf stage_in, stage_out;  // host-API staging
   float eps4 = 1.001e-5f, eps2 = 1e-5f;  // BN epsilons (blob header may override)
-  bool no_win = false;         // VOXEMB_NO_WIN=1: disable conv_win (A/B testing)
-  int win_cin = 0;             // VOXEMB_WIN_CIN=c: conv_win only for Cin == c (debug)
-  bool no_rr = false;          // VOXEMB_NO_RR=1: disable conv1x1_rr
-  bool no_gemm = false;        // VOXEMB_NO_GEMM=1: disable gemm1x1_lds
-  bool no_gemm_pipe = false;   // VOXEMB_NO_GEMM_PIPE=1: gemm1x1_lds instead of gemm1x1_pipe
-  bool no_gemm_wide = false;   // VOXEMB_NO_GEMM_WIDE=1: gemm1x1_pipe instead of gemm1x1_wide
-  bool no_wblk = false;        // VOXEMB_NO_WBLK=1: gemm1x1_ws reads the paired-row weights
-  bool no_s2_fused = false;    // VOXEMB_NO_S2_FUSED=1: 1x1a + split_s2_rows instead of s2_fused
-  bool no_chain_fused = false; // VOXEMB_NO_CHAIN_FUSED=1: 1x1a + chain_rows instead of chain_fused
-  // VOXEMB_CONV3_WIN=1: window-staged conv3x3_win for the w=96 stride-1 branches
-  // (bitwise equal; measured 115 us vs conv3x3_pipe's 97 us per L3 launch at
-  // B=256 -- twice the K-steps, each paying the ring's fixed per-step cost)
-  bool no_conv3_win = true;
-  bool no_conv3_rw = false;    // VOXEMB_NO_CONV3_RW=1: conv3x3_pipe for the w = 96 stride-1 branches
-  bool no_conv3_utt = false;   // VOXEMB_NO_CONV3_UTT=1: conv3x3_pipe for the w = 192 stride-1 branches
-  bool no_conv3_s2r = false;   // VOXEMB_NO_CONV3_S2R=1: conv3x3_pipe for the w = 96 stride-2 branches
-  bool no_gconv = false;       // VOXEMB_NO_GCONV=1: grouped 3x3 on the generic implicit GEMM
-  bool no_conv3 = false;
-  bool no_gemm_pro = false;    // VOXEMB_NO_GEMM_PRO=1: prologue 1x1 convs off the LDS-DMA GEMMs
-  bool no_gemm_taps = false;   // VOXEMB_NO_GEMM_TAPS=1: TDNN dilated convs off gemm1x1_ws
-  bool no_smallk = false;      // VOXEMB_NO_SMALLK=1: DPN 10-channel 1x1s on the generic conv
-  int pro_min_cout = 192;      // VOXEMB_PRO_MIN_COUT: narrowest prologue 1x1 on gemm1x1_ws
-  int num_cu = 256;            // compute units (persistent grids)
-  int gemm_var = 0;            // VOXEMB_GEMM_VAR: gemm1x1_pipe variant (A/B experiments)
-  int gemm_min_k = 128;        // VOXEMB_GEMM_MIN_K: smallest K routed to the LDS GEMMs (the K = 128
-                               // L2 projection: gemm1x1_ws 0.17 ms vs conv1x1_rr 0.26 ms)
-  bool no_chain = false;       // VOXEMB_NO_CHAIN=1: unfused Res2Net branches
-  bool no_stem = false;        // VOXEMB_NO_STEM=1: stem through the generic conv
-  bool no_bneck = false;       // VOXEMB_NO_BNECK=1: unfused identity bottlenecks
-  bool no_chain_rows = false;  // VOXEMB_NO_CHAIN_ROWS=1: row-tiled split_chain instead
-  bool no_split_s2 = false;    // VOXEMB_NO_SPLIT_S2=1: stride-2 branches as separate convs
-  int bneck_nseg = 0;          // VOXEMB_BNECK_NSEG: force row segments per utterance (tests)
-  int bneck_dbg = 0;           // VOXEMB_BNECK_DBG: timing experiments (skips work; wrong results)
-  int chain_r = 0, chain_wpx = 0, chain_nw = 0;  // VOXEMB_CHAIN_R / VOXEMB_CHAIN_WPX (tuning)
-  int rr_wpx = 0, rr_wco = 0;  // VOXEMB_RR_WPX / VOXEMB_RR_WCO: tile overrides (tuning)
+  // Plan switches: kernel-routing A/B and parity knobs, 0 = the product plan.
+  // Read once at load from the environment through kPlanEnv (below); each
+  // names the kernel it turns off and the path taken instead.
+  int no_win = 0;          // VOXEMB_NO_WIN: conv_win off (generic implicit GEMM)
+  int no_rr = 0;           // VOXEMB_NO_RR: conv1x1_rr off
+  int no_gemm = 0;         // VOXEMB_NO_GEMM: the LDS GEMMs off (conv1x1_rr)
+  int no_gemm_pipe = 0;    // VOXEMB_NO_GEMM_PIPE: gemm1x1_lds instead of gemm1x1_pipe
+  int no_gemm_wide = 0;    // VOXEMB_NO_GEMM_WIDE: gemm1x1_pipe instead of gemm1x1_ws
+  int no_wblk = 0;         // VOXEMB_NO_WBLK: gemm1x1_ws reads the paired-row weights
+  int no_s2_fused = 0;     // VOXEMB_NO_S2_FUSED: 1x1a + split_s2_rows instead of s2_fused
+  int no_chain_fused = 0;  // VOXEMB_NO_CHAIN_FUSED: 1x1a + chain_rows instead of chain_fused
+  int no_conv3_rw = 0;     // VOXEMB_NO_CONV3_RW: conv3x3_pipe for the w = 96 stride-1 branches
+  int no_conv3_utt = 0;    // VOXEMB_NO_CONV3_UTT: conv3x3_pipe for the w = 192 stride-1 branches
+  int no_conv3_s2r = 0;    // VOXEMB_NO_CONV3_S2R: conv3x3_pipe for the w = 96 stride-2 branches
+  int no_gconv = 0;        // VOXEMB_NO_GCONV: grouped 3x3 on the generic implicit GEMM
+  int no_conv3 = 0;        // VOXEMB_NO_CONV3: every 3x3 branch kernel off
+  int no_gemm_pro = 0;     // VOXEMB_NO_GEMM_PRO: prologue 1x1 convs off the LDS-DMA GEMMs
+  int no_gemm_taps = 0;    // VOXEMB_NO_GEMM_TAPS: TDNN dilated convs off gemm1x1_ws
+  int no_smallk = 0;       // VOXEMB_NO_SMALLK: DPN 10-channel 1x1s on the generic conv
+  int pro_min_cout = 192;  // VOXEMB_PRO_MIN_COUT: narrowest prologue 1x1 on gemm1x1_ws
+  int gemm_var = 0;        // VOXEMB_GEMM_VAR: -1 = gemm1x1_wide instead of gemm1x1_ws
+                           // (bitwise A/B); other values are diagnostics (VOX_DIAG builds)
+  int gemm_min_k = 128;    // VOXEMB_GEMM_MIN_K: smallest K routed to the LDS GEMMs (the K = 128
+                           // L2 projection: gemm1x1_ws 0.17 ms vs conv1x1_rr 0.26 ms)
+  int no_chain = 0;        // VOXEMB_NO_CHAIN: unfused Res2Net branches
+  int no_stem = 0;         // VOXEMB_NO_STEM: stem through the generic conv
+  int no_bneck = 0;        // VOXEMB_NO_BNECK: unfused identity bottlenecks
+  int no_chain_rows = 0;   // VOXEMB_NO_CHAIN_ROWS: row-tiled split_chain instead
+  int no_split_s2 = 0;     // VOXEMB_NO_SPLIT_S2: stride-2 branches as separate convs
+  int bneck_nseg = 0;      // VOXEMB_BNECK_NSEG: force row segments per utterance (tests)
+  int bneck_dbg = 0;       // VOXEMB_BNECK_DBG: diagnostics (VOX_DIAG builds; skips work)
+  int num_cu = 256;        // compute units (persistent grids)
+};
+
+// environment name -> plan switch (vox_model fields above)
+struct PlanEnv {
+  const char* name;
+  int vox_model::*field;
+};
+static const PlanEnv kPlanEnv[] = {
+    {"VOXEMB_NO_WIN", &vox_model::no_win},
+    {"VOXEMB_NO_RR", &vox_model::no_rr},
+    {"VOXEMB_NO_GEMM", &vox_model::no_gemm},
+    {"VOXEMB_NO_GEMM_PIPE", &vox_model::no_gemm_pipe},
+    {"VOXEMB_NO_GEMM_WIDE", &vox_model::no_gemm_wide},
+    {"VOXEMB_NO_WBLK", &vox_model::no_wblk},
+    {"VOXEMB_NO_S2_FUSED", &vox_model::no_s2_fused},
+    {"VOXEMB_NO_CHAIN_FUSED", &vox_model::no_chain_fused},
+    {"VOXEMB_NO_CONV3_RW", &vox_model::no_conv3_rw},
+    {"VOXEMB_NO_CONV3_UTT", &vox_model::no_conv3_utt},
+    {"VOXEMB_NO_CONV3_S2R", &vox_model::no_conv3_s2r},
+    {"VOXEMB_NO_GCONV", &vox_model::no_gconv},
+    {"VOXEMB_NO_CONV3", &vox_model::no_conv3},
+    {"VOXEMB_NO_GEMM_PRO", &vox_model::no_gemm_pro},
+    {"VOXEMB_NO_GEMM_TAPS", &vox_model::no_gemm_taps},
+    {"VOXEMB_NO_SMALLK", &vox_model::no_smallk},
+    {"VOXEMB_PRO_MIN_COUT", &vox_model::pro_min_cout},
+    {"VOXEMB_GEMM_VAR", &vox_model::gemm_var},
+    {"VOXEMB_GEMM_MIN_K", &vox_model::gemm_min_k},
+    {"VOXEMB_NO_CHAIN", &vox_model::no_chain},
+    {"VOXEMB_NO_STEM", &vox_model::no_stem},
+    {"VOXEMB_NO_BNECK", &vox_model::no_bneck},
+    {"VOXEMB_NO_CHAIN_ROWS", &vox_model::no_chain_rows},
+    {"VOXEMB_NO_SPLIT_S2", &vox_model::no_split_s2},
+    {"VOXEMB_BNECK_NSEG", &vox_model::bneck_nseg},
+    {"VOXEMB_BNECK_DBG", &vox_model::bneck_dbg},
 };
 
 static size_t esize(DType t) { return t == BF16 ? 2 : 4; }
@@ -637,8 +668,6 @@ static void emit_conv(Builder& B, const ConvW& cw, Act x, const void* x2, int ld
     // enough waves: pixel tiles x cout ranges >= ~2048 blocks' worth
     int wpx = conv1x1_rr_max_wpx(ks_rr);
     while (wpx > 1 && (M + 64 * wpx - 1) / (64 * wpx) < 1024) wpx /= 2;
-    if (B.m->rr_wpx > 0) wpx = std::min(wpx, B.m->rr_wpx);
-    if (B.m->rr_wco > 0 && (cw.coutp / 16) % B.m->rr_wco == 0) op.cl.wco = B.m->rr_wco;
     op.cl.wpx = wpx;
     const int gx = (M + 64 * wpx - 1) / (64 * wpx);
     const int tiles = cw.coutp / 16;
@@ -717,7 +746,7 @@ static void emit_conv(Builder& B, const ConvW& cw, Act x, const void* x2, int ld
   // stride 2 only pays off for wide inputs (measured: L4 yes, L2/L3 no)
   if (op.type == 0 && B.m->dt == BF16 && dt_override != F32 && cw.wtc && sh == sw &&
       (sh == 1 || (sh == 2 && cw.cin >= 192)) && !in_mean && !(flags & EPI_PARTIAL) &&
-      !B.m->no_win && (!B.m->win_cin || B.m->win_cin == cw.cin)) {
+      !B.m->no_win) {
     const int taps = cw.kh * cw.kw;
     const int minoff = -(ph * x.W + pw);
     const int maxoff = ((cw.kh - 1) * dh - ph) * x.W + (cw.kw - 1) * dw - pw;
@@ -1178,21 +1207,20 @@ static int build_res2net(Builder& B, const float* x, int n, int t, float* out) {
         q.wstr = wu * 16;
         const long fixed = (long)16 * b0.wco * q.wstr + (q.kcp / 8) * 4;
         int R = 0;
-        const int nthreads = 64 * (m->chain_nw > 0 ? m->chain_nw : 8);
+        const int nthreads = 64 * 8;
         for (int r = 16; r >= 1; --r) {
           const long buf = (long)(r + 2 * q.nst) * (W + 2) * q.astr;
           // the next input x_{k+1} (r + 2*(nst-1) rows) is prefetched into 8 chunks/thread
           const long xchunks = (long)(r + 2 * (q.nst - 1)) * W * (w / 8);
           if (2 * buf + fixed <= 160 * 1024 && xchunks <= 8L * nthreads) { R = r; break; }
         }
-        if (m->chain_r > 0) R = std::min(R, m->chain_r);
         // register-prefetched weights: the kernel holds enough chunks for w <= 16*wco;
         // keep the widest tile counts (wco 6) out (too many registers)
         bool ok = R > 0 && s - 1 <= 8 && b0.wtc && b0.wco <= 4 && w <= 16 * b0.wco;
         for (int j = 0; ok && j < s - 1; ++j) ok = m->convs[ci + j].wtc != nullptr;
         if (ok) {
           q.R = R;
-          q.nwaves = m->chain_nw > 0 ? m->chain_nw : 8;
+          q.nwaves = 8;
           q.buf_bytes = (R + 2 * q.nst) * (W + 2) * q.astr;
           q.lds = (int)(2L * q.buf_bytes + fixed);
           double fl = 0;
@@ -1208,7 +1236,7 @@ static int build_res2net(Builder& B, const float* x, int n, int t, float* out) {
           op.type = 10;
           op.ch = q;
           op.cl.wco = b0.wco;
-          op.cl.wpx = m->chain_wpx > 0 ? m->chain_wpx : (b0.wco <= 2 ? 4 : 2);  // wco 3 spills at 4
+          op.cl.wpx = b0.wco <= 2 ? 4 : 2;  // wco 3 spills at 4
           op.flops = fl;
           op.bytes = (double)es * n * H * W * w * (2.0 * (s - 1));
           B.ops->push_back(op);
@@ -1272,10 +1300,8 @@ static int build_res2net(Builder& B, const float* x, int n, int t, float* out) {
           p.kh = br.kh; p.kw = br.kw; p.sh = p.sw = stride; p.dh = p.dw = 1; p.ph = p.pw = 1;
           p.groups = br.groups; p.flags = EPI_AFFINE | EPI_RELU;
           ok = br.wtc && br.mean && br.cin == w && br.cout == w && conv3_pipe_ok(p);
-          // stride-1 w = 96: input window staged once per tile (conv3w.hip)
-          if (ok && !m->no_conv3_win && conv3_win_ok(p)) op.type = 23;
-          // ... or with the weights in registers (conv3r.hip)
-          else if (ok && !m->no_conv3_rw && conv3_rw_ok(p)) op.type = 25;
+          // stride-1 w = 96: weights in registers, window staged once per tile (conv3r.hip)
+          if (ok && !m->no_conv3_rw && conv3_rw_ok(p)) op.type = 25;
           // w = 192: one utterance band's window staged once, weights streamed (conv3u.hip)
           else if (ok && !m->no_conv3_utt && conv3_utt_ok(p)) op.type = 26;
           // stride 2, w = 96: register weights, 3-row window tiles (conv3s.hip)
@@ -1490,7 +1516,6 @@ static hipError_t run_op(vox_model* m, const Op& op, hipStream_t s) {
     case 14: return launch_split_s2(op.ch, s);
     case 22: return launch_s2_fused(op.ch, s);
     case 24: return launch_chain_fused(op.ch, s);
-    case 23: return launch_conv3_win(op.cp, m->num_cu, s);
     case 25: return launch_conv3_rw(op.cp, m->num_cu, s);
     case 26: return launch_conv3_utt(op.cp, m->num_cu, s);
     case 27: return launch_conv1x1_smallk(op.cp, s);
@@ -1560,40 +1585,17 @@ extern "C" int vox_load_blob(const void* blob, size_t nbytes, int device, int pr
   m->expand_dim = spec.geti("expand_dim", 3);
   if (!spec.get("bn_eps_4d").empty()) m->eps4 = std::strtof(spec.get("bn_eps_4d").c_str(), nullptr);
   if (!spec.get("bn_eps_2d").empty()) m->eps2 = std::strtof(spec.get("bn_eps_2d").c_str(), nullptr);
-  if (const char* e = std::getenv("VOXEMB_NO_WIN")) m->no_win = std::atoi(e) != 0;
-  if (const char* e = std::getenv("VOXEMB_WIN_CIN")) m->win_cin = std::atoi(e);
-  if (const char* e = std::getenv("VOXEMB_NO_RR")) m->no_rr = std::atoi(e) != 0;
-  if (const char* e = std::getenv("VOXEMB_RR_WPX")) m->rr_wpx = std::atoi(e);
-  if (const char* e = std::getenv("VOXEMB_NO_GEMM")) m->no_gemm = std::atoi(e) != 0;
-  if (const char* e = std::getenv("VOXEMB_NO_GEMM_PIPE")) m->no_gemm_pipe = std::atoi(e) != 0;
-  if (const char* e = std::getenv("VOXEMB_NO_GEMM_WIDE")) m->no_gemm_wide = std::atoi(e) != 0;
-  if (const char* e = std::getenv("VOXEMB_NO_WBLK")) m->no_wblk = std::atoi(e) != 0;
   if (const char* e = std::getenv("VOXEMB_NO_GRAPH")) m->use_graph = std::atoi(e) == 0;
-  if (const char* e = std::getenv("VOXEMB_NO_GCONV")) m->no_gconv = std::atoi(e) != 0;
-  if (const char* e = std::getenv("VOXEMB_NO_CONV3")) m->no_conv3 = std::atoi(e) != 0;
-  if (const char* e = std::getenv("VOXEMB_NO_GEMM_PRO")) m->no_gemm_pro = std::atoi(e) != 0;
-  if (const char* e = std::getenv("VOXEMB_NO_GEMM_TAPS")) m->no_gemm_taps = std::atoi(e) != 0;
-  if (const char* e = std::getenv("VOXEMB_NO_SMALLK")) m->no_smallk = std::atoi(e) != 0;
-  if (const char* e = std::getenv("VOXEMB_PRO_MIN_COUT")) m->pro_min_cout = std::atoi(e);
-  if (const char* e = std::getenv("VOXEMB_GEMM_VAR")) m->gemm_var = std::atoi(e);
-  if (const char* e = std::getenv("VOXEMB_GEMM_MIN_K")) m->gemm_min_k = std::atoi(e);
-  if (const char* e = std::getenv("VOXEMB_NO_CHAIN")) m->no_chain = std::atoi(e) != 0;
-  if (const char* e = std::getenv("VOXEMB_NO_STEM")) m->no_stem = std::atoi(e) != 0;
-  if (const char* e = std::getenv("VOXEMB_NO_BNECK")) m->no_bneck = std::atoi(e) != 0;
-  if (const char* e = std::getenv("VOXEMB_NO_CHAIN_ROWS")) m->no_chain_rows = std::atoi(e) != 0;
-  if (const char* e = std::getenv("VOXEMB_NO_SPLIT_S2")) m->no_split_s2 = std::atoi(e) != 0;
-  if (const char* e = std::getenv("VOXEMB_NO_S2_FUSED")) m->no_s2_fused = std::atoi(e) != 0;
-  if (const char* e = std::getenv("VOXEMB_NO_CHAIN_FUSED")) m->no_chain_fused = std::atoi(e) != 0;
-  if (const char* e = std::getenv("VOXEMB_CONV3_WIN")) m->no_conv3_win = std::atoi(e) == 0;
-  if (const char* e = std::getenv("VOXEMB_NO_CONV3_RW")) m->no_conv3_rw = std::atoi(e) != 0;
-  if (const char* e = std::getenv("VOXEMB_NO_CONV3_UTT")) m->no_conv3_utt = std::atoi(e) != 0;
-  if (const char* e = std::getenv("VOXEMB_NO_CONV3_S2R")) m->no_conv3_s2r = std::atoi(e) != 0;
-  if (const char* e = std::getenv("VOXEMB_BNECK_NSEG")) m->bneck_nseg = std::atoi(e);
-  if (const char* e = std::getenv("VOXEMB_BNECK_DBG")) m->bneck_dbg = std::atoi(e);
-  if (const char* e = std::getenv("VOXEMB_CHAIN_R")) m->chain_r = std::atoi(e);
-  if (const char* e = std::getenv("VOXEMB_CHAIN_WPX")) m->chain_wpx = std::atoi(e);
-  if (const char* e = std::getenv("VOXEMB_CHAIN_NW")) m->chain_nw = std::atoi(e);
-  if (const char* e = std::getenv("VOXEMB_RR_WCO")) m->rr_wco = std::atoi(e);
+  for (const PlanEnv& pe : kPlanEnv)
+    if (const char* e = std::getenv(pe.name)) m.get()->*pe.field = std::atoi(e);
+#ifndef VOX_DIAG
+  // diagnostic variants skip work (wrong results) and are compiled only into
+  // the VOX_DIAG build (libvoxemb_diag.so, build_native.py --diag)
+  if (m->bneck_dbg || (m->gemm_var != 0 && m->gemm_var != 1 && m->gemm_var != -1) ||
+      std::getenv("VOXEMB_CONV3_RW_DBG"))
+    return fail(VOX_EINVAL, "diagnostic switches (VOXEMB_BNECK_DBG / VOXEMB_GEMM_VAR / "
+                            "VOXEMB_CONV3_RW_DBG) need the VOX_DIAG build (libvoxemb_diag.so)");
+#endif
   if ((rc = load_weights(m.get(), ts))) return rc;
   HIPCHK(hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking));
   HIPCHK(hipEventCreateWithFlags(&m->done, hipEventDisableTiming));
@@ -1767,8 +1769,6 @@ extern "C" int vox_profile(vox_model* m, const float* d_x, int n, int t, int f, 
         tag |= (1 << 30) | ((m->gemm_var == 0 || m->gemm_var == 1) ? (1 << 17) : 0);
       else if (o.type == 22)
         tag |= (1 << 26) | (1 << 19);
-      else if (o.type == 23)
-        tag |= (1 << 29) | (1 << 19);
       else if (o.type == 24)
         tag |= (1 << 25) | (1 << 19);
       else if (o.type == 25)
@@ -1807,13 +1807,13 @@ extern "C" int vox_plan_describe(vox_model* m, const float* d_x, int n, int t, i
   static const char* tn[] = {"igemm", "reduce", "pool", "avgpool", "convert", "igemm32", "bnrelu",
                              "win", "rr", "gemm", "chain", "stem", "bneck", "chainrows", "splits2",
                              "cvt16", "atttanh", "attpool", "gemmpipe", "gconv", "conv3pipe",
-                             "gemmwide", "s2fused", "conv3win", "chainfused", "conv3rw", "conv3utt",
+                             "gemmwide", "s2fused", "-", "chainfused", "conv3rw", "conv3utt",
                              "smallk", "conv3s2r"};
   for (const Op& o : m->plan) {
     char line[256];
     const ConvParams& p = o.cp;
     if (o.type == 0 || o.type == 5 || o.type == 7 || o.type == 8 || o.type == 9 || o.type == 18 ||
-        o.type == 20 || o.type == 21 || o.type == 23 || o.type == 25 || o.type == 26 ||
+        o.type == 20 || o.type == 21 || o.type == 25 || o.type == 26 ||
         o.type == 27 || o.type == 28)
       std::snprintf(line, sizeof(line),
                     "%s wco=%d wpx=%d s=%d N=%d H=%d W=%d Cin=%d Ho=%d Wo=%d Cout=%d k=%dx%d st=%d "

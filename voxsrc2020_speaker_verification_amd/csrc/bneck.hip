@@ -198,15 +198,17 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
   // ---- input rows: global -> registers (prefetch) -> LDS
   // two register sets for the input rows: a row is requested two steps before
   // it is used (HBM latency under load exceeds a step)
-  vu32x4 inr[2][K::IREG];
+  vu32x4 inr[2][K::IREG] = {};
   const int nres = is_c ? PT : 0;                               // residual loads per step
-  const int nst = ((q.dbg & 256) && blockIdx.x == 0) ? 1 : 0;  // trace stamps (stores)
-  // Every global access of the row loop is issued as inline asm with the
-  // wave's vmcnt counted by hand (device_common.h vld16 / vst16 / vm_wait):
-  // compiler-placed waits fell back to vmcnt(0) before the staging writes,
-  // holding every wave on its in-flight 1x1c stores and residual prefetches.
-  // Each load is always issued (rows outside the image read a zero line), so
-  // the per-step op counts are wave-uniform:
+  const int nst = ((VOX_DBG(q) & 256) && blockIdx.x == 0) ? 1 : 0;  // trace stamps (stores)
+  // The row loop's stores are inline asm and its waits counted by hand
+  // (device_common.h vst16 / vm_wait): compiler-placed waits fell back to
+  // vmcnt(0) before the staging writes, holding every wave on its in-flight
+  // 1x1c stores and residual prefetches.  The loads are ordinary loads
+  // (vld16), so the compiler's own waits also cover every use and copy of
+  // their destinations (tests/test_vmcnt_audit.py).  Each load is always
+  // issued (rows outside the image read a zero line), so the per-step op
+  // counts are wave-uniform:
   //   phase 0: 1x1c waves: ns stores (PT when row c is owned, else 0) then PT
   //            residual loads (row c+1); phase 1: IREG input loads (row a+3).
   const bf16_t* zline = reinterpret_cast<const bf16_t*>(g_vox_zero);
@@ -216,7 +218,7 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
       int c = tid + i * NT;
       const int px = c / K::CU, u = c - px * K::CU;
       const bool ok = c < 16 * PT * K::CU && px < W && r >= 0 && r < H;
-      inr[P][i] = vld16(ok ? (const void*)(X + (img + (size_t)r * W + px) * CI + u * 8) : zline);
+      vld16(inr[P][i], ok ? (const void*)(X + (img + (size_t)r * W + px) * CI + u * 8) : zline);
     }
   };
   auto store_in = [&](auto P) __attribute__((always_inline)) {
@@ -230,7 +232,7 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
   };
   // the residual row is requested one step ahead (a second register set would
   // push the chain's fragment reads onto the registers they are consumed from)
-  vu32x4 resb[PT];
+  vu32x4 resb[PT] = {};
   auto load_res = [&](int r) __attribute__((always_inline)) {
     if (!is_c) return;
 #pragma unroll
@@ -240,7 +242,7 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
       // the (CI = 32)-channel input row, for the shortcut MFMAs
       const int cho = K::PROJ ? 8 * g : 32 * pq + 8 * g;
       const bool ok = r >= h0 && r < h1 && px < W;
-      resb[j] = vld16(ok ? (const void*)(X + (img + (size_t)r * W + px) * CI + cho) : zline);
+      vld16(resb[j], ok ? (const void*)(X + (img + (size_t)r * W + px) * CI + cho) : zline);
     }
   };
 
@@ -268,7 +270,7 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
 
   // step t (register set P = t & 1): input row a + 1 was requested two steps
   // earlier, residual row c one step earlier
-  const bool trace = (q.dbg & 256) && blockIdx.x == 0 && lane == 0;
+  const bool trace = (VOX_DBG(q) & 256) && blockIdx.x == 0 && lane == 0;
   auto stamp = [&](int t, int i) __attribute__((always_inline)) {
     if (trace && t < 512) g_vox_trace[(wave * 512 + t) * 4 + i] = __builtin_amdgcn_s_memtime();
   };
@@ -276,11 +278,11 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
     const int a = a0 + t;
     const int c = a - K::LAG_C;
     auto& res = resb;
-    const bool cstep = is_c && c >= h0 && c < h1 && !(q.dbg & 2);
+    const bool cstep = is_c && c >= h0 && c < h1 && !(VOX_DBG(q) & 2);
     const int ns_cur = cstep ? PT : 0;
     stamp(t, 0);
     // ---------------- phase 0: 1x1a (row a) | 1x1c (row c)
-    if (is_a && !(q.dbg & 1)) {
+    if (is_a && !(VOX_DBG(q) & 1)) {
       const bool inimg = a >= 0 && a < H;
       const int ch = 32 * pq + 8 * g;
       const int p = ch / WID, off = ch - p * WID;
@@ -415,12 +417,12 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
 #pragma unroll
       for (int j = 0; j < PT; ++j) vm_launder(res[j]);
     }
-    if (!(q.dbg & 8)) load_res(c + 1);
+    if (!(VOX_DBG(q) & 8)) load_res(c + 1);
     stamp(t, 1);
     __syncthreads();
     stamp(t, 2);
     // ---------------- phase 1: all 3x3 stages, stage k on row a-2k+1
-    if (!(q.dbg & 8)) {
+    if (!(VOX_DBG(q) & 8)) {
       // input row a+1 (loaded at step t-2): younger are step t-1's and this
       // step's stores and residual loads, step t-1's input loads, 8 stamps
       vm_wait(t < 2 ? 0 : K::IREG + ns_prev + ns_cur + 2 * nres + 8 * nst);
@@ -428,7 +430,7 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
       load_in(P, a + 3);
     }
     ns_prev = ns_cur;
-    if (chain_wave && !(q.dbg & 4)) {
+    if (chain_wave && !(VOX_DBG(q) & 4)) {
       const int k = ck;
       const int co = 16 * ci + 4 * g;
       const int r = a - 2 * k + 1;
@@ -945,7 +947,7 @@ __global__ __launch_bounds__((ChainFusedCfg<CI, WID, S, PT>::NT)) void chain_fus
         acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
         bc[j] = frag(0, j);
       }
-      if (!(q.dbg & 128)) {   // (diagnostics: 128 = no phase-A MFMAs)
+      if (!(VOX_DBG(q) & 128)) {   // (diagnostics: 128 = no phase-A MFMAs)
 #pragma unroll
         for (int s = 0; s < K::KSA; ++s) {
           if (s + 1 < K::KSA) {
@@ -980,7 +982,7 @@ __global__ __launch_bounds__((ChainFusedCfg<CI, WID, S, PT>::NT)) void chain_fus
     // ---------------- phase B: chain_rows' stages, stage k on row a-2k+1
     // (VOXEMB_BNECK_DBG diagnostics, garbage out: 16 = wave 8 skips its role,
     // 32 = wave 1 skips its role, 64 = no phase B)
-    if (role && !((q.dbg & 16) && wave == 8) && !((q.dbg & 32) && wave == 1) && !(q.dbg & 64)) {
+    if (role && !((VOX_DBG(q) & 16) && wave == 8) && !((VOX_DBG(q) & 32) && wave == 1) && !(VOX_DBG(q) & 64)) {
       const int k = ck;
       const int co = 16 * ci + 4 * g;
       const int r = a - 2 * k + 1;
@@ -1456,11 +1458,10 @@ __global__ __launch_bounds__((S2FusedCfg<CI, WID, S, WIN>::NT)) void s2_fused(Ch
   }
 
   // two input rows per step: global -> registers (one step ahead) -> LDS.
-  // The row loads are inline asm (device_common.h vld16; rows outside the
-  // image read a zero line) and waited for by hand right after the phase-A
-  // barrier, where only they and the previous step's output stores are in
-  // flight: compiler-placed waits drained them at the top of phase A.
-  vu32x4 xr[K::XREG];
+  // The row loads (device_common.h vld16; rows outside the image read a zero
+  // line) are waited for by hand right after the phase-A barrier, where only
+  // they and the previous step's output stores are in flight.
+  vu32x4 xr[K::XREG] = {};
   const int ldx = q.ldx;
   const bf16_t* zline = reinterpret_cast<const bf16_t*>(g_vox_zero);
   auto load_x = [&](int r0) __attribute__((always_inline)) {
@@ -1473,7 +1474,7 @@ __global__ __launch_bounds__((S2FusedCfg<CI, WID, S, WIN>::NT)) void s2_fused(Ch
       const int px = cc / CU, u = cc - px * CU;
       const int r = r0 + rr;
       const bool ok = rr < 2 && r >= 0 && r < H;
-      xr[i] = vld16(ok ? (const void*)(base + (rr * W + px) * ldx + u * 8) : zline);
+      vld16(xr[i], ok ? (const void*)(base + (rr * W + px) * ldx + u * 8) : zline);
     }
   };
   auto store_x = [&]() __attribute__((always_inline)) {
@@ -1499,9 +1500,9 @@ __global__ __launch_bounds__((S2FusedCfg<CI, WID, S, WIN>::NT)) void s2_fused(Ch
   store_x();
   __syncthreads();
   for (int ho = g0 - 1; ho < g1; ++ho) {
-    if (!(q.dbg & 8)) load_x(2 * ho + 2);   // lands during this step, goes to LDS at its end
+    if (!(VOX_DBG(q) & 8)) load_x(2 * ho + 2);   // lands during this step, goes to LDS at its end
     // ---------------- phase A: 1x1a rows 2ho, 2ho+1 -> ring
-    if (!(q.dbg & 1)) {
+    if (!(VOX_DBG(q) & 1)) {
       const int ch = 32 * (t16 >> 1) + 8 * g + 4 * (t16 & 1);
       const int p = ch / WID, off = ch - p * WID;
       const f32x4 m0 = *reinterpret_cast<const f32x4*>(bma + ch);
@@ -1546,12 +1547,12 @@ __global__ __launch_bounds__((S2FusedCfg<CI, WID, S, WIN>::NT)) void s2_fused(Ch
       }
     }
     __syncthreads();
-    if (!(q.dbg & 8)) {   // input rows 2ho+2, 2ho+3: phase A is done with the staging
+    if (!(VOX_DBG(q) & 8)) {   // input rows 2ho+2, 2ho+3: phase A is done with the staging
       vm_wait(0);
       store_x();
     }
     // ---------------- phase B: output row ho from A-rows 2ho-1 .. 2ho+1
-    if (ho >= g0 && !(q.dbg & 2)) {
+    if (ho >= g0 && !(VOX_DBG(q) & 2)) {
       const int rb0 = __builtin_amdgcn_readfirstlane(((2 * ho - 1 + 840) % 3) * ROWB);
       const int rb1 = __builtin_amdgcn_readfirstlane(((2 * ho + 840) % 3) * ROWB);
       const int rb2 = __builtin_amdgcn_readfirstlane(((2 * ho + 1 + 840) % 3) * ROWB);
@@ -1605,7 +1606,7 @@ __global__ __launch_bounds__((S2FusedCfg<CI, WID, S, WIN>::NT)) void s2_fused(Ch
             *reinterpret_cast<bf16x4*>(Bo + (imgo + (size_t)ho * Wo + wo) * q.ldb + ck * WID + co) = y;
           }
         }
-      } else if (!(q.dbg & 4)) {
+      } else if (!(VOX_DBG(q) & 4)) {
         // last split: AvgPool 3x3/2 VALID over the fixed-padded plane, divisor 9
         // (taps outside the image skipped, in the order of avgpool3s2_v8)
         const char* pl = rings + (S - 1) * PLANEB;

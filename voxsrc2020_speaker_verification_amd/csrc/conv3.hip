@@ -60,10 +60,11 @@ __device__ __forceinline__ void c3_glds16(const void* src, uint32_t lds) {
       : "memory");
 }
 
-__device__ __forceinline__ u32x4 c3_gld16(const void* src) {
-  u32x4 v;
-  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(src) : "memory");
-  return v;
+// an ordinary (compiler-visible) load: the compiler's waitcnt pass covers
+// every use and copy of the destination (see device_common.h vld16); the
+// counted wait before the epilogue stays as the place the values are needed
+__device__ __forceinline__ void c3_gld16(u32x4& v, const void* src) {
+  v = *reinterpret_cast<const u32x4*>(src);
 }
 
 // the trailing s_nop keeps the next instruction from overwriting the data
@@ -211,7 +212,7 @@ void conv3x3_pipe(ConvParams p) {
   constexpr int L0 = KT - 1 - LEAD;
   static_assert(L0 >= 0, "K too short for the epilogue lead");
   constexpr int EPI_LD = HAS_Z ? 18 : 12;  // epilogue loads per wave
-  u32x4 bm[3][2], bi[3][2], xz[3][2];
+  u32x4 bm[3][2] = {}, bi[3][2] = {}, xz[3][2] = {};
   for (int s = 0; s < S; ++s) {
     // step s's operands landed; younger: step s+1's DMA, the epilogue loads
     // while they are in flight (steps L0+1 .. KT-1) and, in the two steps
@@ -233,15 +234,15 @@ void conv3x3_pipe(ConvParams p) {
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
         const int ch = co0 + 32 * q + 8 * g;
-        bm[q][0] = c3_gld16(p.mean + ch);
-        bm[q][1] = c3_gld16(p.mean + ch + 4);
-        bi[q][0] = c3_gld16(p.inv + ch);
-        bi[q][1] = c3_gld16(p.inv + ch + 4);
+        c3_gld16(bm[q][0], p.mean + ch);
+        c3_gld16(bm[q][1], p.mean + ch + 4);
+        c3_gld16(bi[q][0], p.inv + ch);
+        c3_gld16(bi[q][1], p.inv + ch + 4);
         if (HAS_Z) {
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
             const int pix = min(px0 + wave * 32 + 16 * j + col, M - 1);
-            xz[q][j] = c3_gld16(XZ + (size_t)pix * p.ldr + ch);
+            c3_gld16(xz[q][j], XZ + (size_t)pix * p.ldr + ch);
           }
         }
       }

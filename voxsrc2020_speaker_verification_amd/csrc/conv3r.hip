@@ -322,14 +322,20 @@ int conv3_rw_ok(const ConvParams& p) {
 
 template <int W, bool Z>
 static void launch_cr(const ConvParams& p, int G, hipStream_t s) {
+#ifdef VOX_DIAG
   static const int dbg = [] {
     const char* e = std::getenv("VOXEMB_CONV3_RW_DBG");
     return e ? std::atoi(e) : 0;
   }();
+#else
+  constexpr int dbg = 0;
+#endif
   switch (dbg) {
+#ifdef VOX_DIAG
 #define CR_L(d) case d: hipLaunchKernelGGL((conv3x3_rw<W, Z, d>), dim3(G), dim3(CR_NT), CrCfg<W>::LDS, s, p); break;
     CR_L(1) CR_L(2) CR_L(8) CR_L(16) CR_L(32) CR_L(24) CR_L(48) CR_L(40)
 #undef CR_L
+#endif
     default: hipLaunchKernelGGL((conv3x3_rw<W, Z, 0>), dim3(G), dim3(CR_NT), CrCfg<W>::LDS, s, p); break;
   }
 }

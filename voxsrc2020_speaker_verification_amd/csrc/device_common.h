@@ -59,10 +59,17 @@ __device__ __forceinline__ bf16x8 relu_bf16(bf16x8 v) {
 // No "memory" clobbers: the kernels never read back what these touch, and a
 // clobber would pin every LDS access around each store.
 typedef unsigned vu32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ vu32x4 vld16(const void* p) {
-  vu32x4 v;
-  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p));
-  return v;
+// The load itself is an ordinary (compiler-visible) global load: the
+// compiler's waitcnt pass then covers every use and every register copy of the
+// destination, so no allocation choice can let a late load land in a register
+// that holds something else (an inline-asm load whose destination the
+// compiler believes written at issue was copied into the loop-carried
+// prefetch buffer before the data arrived in one build -- tools/vmcnt_audit.py).
+// The asm stores below are invisible to that pass, which only makes its
+// counts conservative (it waits for them too), never unsafe; vm_wait /
+// vm_launder keep marking where the kernels expect each load to have landed.
+__device__ __forceinline__ void vld16(vu32x4& v, const void* p) {
+  v = *reinterpret_cast<const vu32x4*>(p);
 }
 // the trailing s_nop keeps the next instruction from overwriting the data
 // registers before the store has read them

@@ -66,10 +66,11 @@ __device__ __forceinline__ void glds16(const void* src, uint32_t lds) {
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ u32x4 gld16(const void* src) {
-  u32x4 v;
-  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(src) : "memory");
-  return v;
+// an ordinary (compiler-visible) load: the compiler's waitcnt pass covers
+// every use and copy of the destination (see device_common.h vld16); the
+// counted wait before the epilogue stays as the place the values are needed
+__device__ __forceinline__ void gld16(u32x4& v, const void* src) {
+  v = *reinterpret_cast<const u32x4*>(src);
 }
 
 // the trailing s_nop keeps the next instruction from overwriting the data
@@ -229,8 +230,8 @@ void gemm1x1_pipe(ConvParams p) {
   constexpr int LEAD = 2;
   const int L0 = KT - 1 - LEAD;
   const int EPI_LD = ((flags & EPI_AFFINE) ? 8 : 0) + ((flags & EPI_RES) ? 8 : 0);
-  u32x4 rv[2][4];
-  u32x4 bm[2][2], bi[2][2];
+  u32x4 rv[2][4] = {};
+  u32x4 bm[2][2] = {}, bi[2][2] = {};
   for (int s = 0; s < S; ++s) {
     // operands of step s landed (this wave's DMA); younger: exactly the ops
     // issued after that DMA -- step s+1's six pieces, the epilogue loads while
@@ -292,16 +293,16 @@ void gemm1x1_pipe(ConvParams p) {
         const int ch = co0 + wm * 64 + 32 * q + 8 * g;
         const int chc = ch < p.Cout ? ch : 0;
         if (flags & EPI_AFFINE) {
-          bm[q][0] = gld16(p.mean + chc);
-          bm[q][1] = gld16(p.mean + chc + 4);
-          bi[q][0] = gld16(p.inv + chc);
-          bi[q][1] = gld16(p.inv + chc + 4);
+          gld16(bm[q][0], p.mean + chc);
+          gld16(bm[q][1], p.mean + chc + 4);
+          gld16(bi[q][0], p.inv + chc);
+          gld16(bi[q][1], p.inv + chc + 4);
         }
         if (flags & EPI_RES) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int pix = min(px0 + wn * 64 + 16 * j + col, M - 1);
-            rv[q][j] = gld16(R + (size_t)pix * p.ldr + chc);
+            gld16(rv[q][j], R + (size_t)pix * p.ldr + chc);
           }
         }
       }
@@ -454,10 +455,12 @@ hipError_t launch_gemm_pipe(const ConvParams& p, int num_cu, int variant, hipStr
                        GP_NST * GP_SLOT + 8 * p.kp, s, p);
   else if (variant == 1)
     hipLaunchKernelGGL((gemm1x1_pipe<0, false>), dim3(G), dim3(GP_NT), GP_NST * GP_SLOT, s, p);
+#ifdef VOX_DIAG
   else if (variant == 2)
     hipLaunchKernelGGL((gemm1x1_pipe<1, false, 1>), dim3(G), dim3(GP_NT), GP_NST * GP_SLOT, s, p);
   else if (variant == 3)
     hipLaunchKernelGGL((gemm1x1_pipe<1, false, 2>), dim3(G), dim3(GP_NT), GP_NST * GP_SLOT, s, p);
+#endif
   else
     hipLaunchKernelGGL((gemm1x1_pipe<1, false>), dim3(G), dim3(GP_NT), GP_NST * GP_SLOT, s, p);
   return hipGetLastError();

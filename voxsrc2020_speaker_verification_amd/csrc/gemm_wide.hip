@@ -361,7 +361,8 @@ constexpr int GS_NL = 4;   // loader waves
 // BM = pixels per tile: 256, or 192 for the 256-wide tiles (their compute waves
 // then hold 96 accumulators and fit the cap; the residual takes 3 phases)
 // DBG (diagnostics, VOXEMB_GEMM_VAR 21/22): 1 = compute waves skip fragment
-// reads and MFMAs (stores kept), 2 = loaders issue no DMA; results garbage
+// reads and MFMAs (stores kept), 2 = loaders issue no DMA, 8 = loaders skip
+// the weight pieces (operand + residual DMA only); results garbage
 // MODE (operand variants; 0 = the Res2Net 1x1s):
 //   GS_PRO : BN + ReLU prologue on the B fragments, relu((x - m[k]) * inv[k])
 //            rounded to bf16, as gemm1x1_pipe<.., PRO> (DPN bn_relu_conv,
@@ -498,9 +499,10 @@ __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
             const int hi = tho[i] + sh_t;
             a = (hi >= 0 && hi < p.H) ? src[i] + (size_t)hi * p.ldx + ci0 : zero;
           }
-          if (!(DBG & 2)) gw_glds16(a, lds0 + (uint32_t)slot * GW_SLOT + (uint32_t)gi * 1024u);
+          if (!(DBG & 2) && !((DBG & 8) && i < BN / 64))
+            gw_glds16(a, lds0 + (uint32_t)slot * GW_SLOT + (uint32_t)gi * 1024u);
         }
-        n = (DBG & 2) ? 0 : NLL;
+        n = (DBG & 2) ? 0 : (DBG & 8) ? NLL - BN / 64 : NLL;
       } else if (RES) {
         // residual phase ph: slot row r (512 B) = pixel l_px0 + (BM/4) (r / 16) + 16 ph + r % 16
         const int ph = l_k - KT;
@@ -744,7 +746,7 @@ hipError_t launch_gemm_wide(const ConvParams& p0, int num_cu, int variant, hipSt
   // VOXEMB_GEMM_VAR=-1 selects gemm1x1_wide
   if (variant == 0) variant = 1;
   if (variant == -1) variant = 0;
-  if (variant == 1 || (variant >= 21 && variant <= 25)) {   // wave-specialised
+  if (variant == 1 || (variant >= 21 && variant <= 29)) {   // wave-specialised
     auto go = [&](auto dbgc) {
       constexpr int D = decltype(dbgc)::value;
       if (bn == 192) {
@@ -760,14 +762,20 @@ hipError_t launch_gemm_wide(const ConvParams& p0, int num_cu, int variant, hipSt
           hipLaunchKernelGGL((gemm1x1_ws<256, false, 192, D>), dim3(G2), dim3(GS_NT), lds, s, p);
       }
     };
+#ifdef VOX_DIAG
     if (variant == 21) go(std::integral_constant<int, 1>{});
     else if (variant == 22) go(std::integral_constant<int, 2>{});
     else if (variant == 25) go(std::integral_constant<int, 5>{});
     else if (variant == 24) go(std::integral_constant<int, 4>{});
-    else go(std::integral_constant<int, 0>{});
+    else if (variant == 28) go(std::integral_constant<int, 8>{});
+    else if (variant == 29) go(std::integral_constant<int, 9>{});
+    else
+#endif
+      go(std::integral_constant<int, 0>{});
     return hipGetLastError();
   }
   switch (variant) {   // 0 = the product kernel; 11..17 = diagnostics (DBG = variant - 10)
+#ifdef VOX_DIAG
     case 11: launch_wide_t<1>(p, bn, G, lds, s); break;
     case 12: launch_wide_t<2>(p, bn, G, lds, s); break;
     case 14: launch_wide_t<4>(p, bn, G, lds, s); break;
@@ -776,6 +784,7 @@ hipError_t launch_gemm_wide(const ConvParams& p0, int num_cu, int variant, hipSt
     case 42: launch_wide_t<32>(p, bn, G, lds, s); break;
     case 74: launch_wide_t<64>(p, bn, G, lds, s); break;
     case 15: launch_wide_t<5>(p, bn, G, lds, s); break;
+#endif
     default: launch_wide_t<0>(p, bn, G, lds, s); break;
   }
   return hipGetLastError();

@@ -3,6 +3,16 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// Diagnostic variants (parts of a kernel skipped for timing; wrong results) are
+// compiled only into the VOX_DIAG build (build_native.py --diag ->
+// libvoxemb_diag.so); in the product library VOX_DBG(q) is a constant 0 and
+// those paths do not exist.
+#ifdef VOX_DIAG
+#define VOX_DBG(q) ((q).dbg)
+#else
+#define VOX_DBG(q) 0
+#endif
+
 namespace vox {
 
 enum DType { F32 = 0, BF16 = 1 };
@@ -65,6 +75,7 @@ struct ChainParams {
   const void* x; int ldx; int cin;
   const void* wa; const float* ma; const float* ia;
   int dbg;                          // diagnostics (VOXEMB_BNECK_DBG): skip parts, garbage out
+                                    // (read only in VOX_DIAG builds, see VOX_DBG)
 };
 hipError_t launch_split_chain(const ChainParams& q, int wco, int wpx, hipStream_t s);
 // Row-streamed split chain (bneck.hip): utterance segments of q.R rows, q.nwaves
@@ -127,8 +138,6 @@ hipError_t launch_gemm1x1(const ConvParams& p, hipStream_t s);
 // one workgroup per CU.  gemm_pipe_ok: K % 64 == 0, K >= 192, coutp % 128 == 0.
 int gemm_pipe_ok(const ConvParams& p);
 hipError_t launch_gemm_pipe(const ConvParams& p, int num_cu, int variant, hipStream_t s);
-// Window-staged 3x3 (conv3w.hip) for the w = 96 stride-1 branches at image
-// width 20 or 10: same tiles / epilogue / bits as conv3x3_pipe.
 // Register-weight 3x3 (conv3r.hip): w = 96 stride-1 branches, weights in
 // registers, the input window staged once per 128-pixel tile.
 int conv3_rw_ok(const ConvParams& p);
@@ -141,8 +150,6 @@ hipError_t launch_conv3_utt(const ConvParams& p, int num_cu, hipStream_t s);
 // staged once in LDS.
 int conv3_s2r_ok(const ConvParams& p);
 hipError_t launch_conv3_s2r(const ConvParams& p, int num_cu, hipStream_t s);
-int conv3_win_ok(const ConvParams& p);
-hipError_t launch_conv3_win(const ConvParams& p, int num_cu, hipStream_t s);
 // Wide-tile variant (gemm_wide.hip): 256 x BN tiles, BN = 256 (Cout % 256 == 0)
 // or 192 (Cout % 192 == 0, no residual), K % 32 == 0, K >= 96, no prologue.
 // gemm_wide_bn returns BN or 0 when it does not apply.
