@@ -199,7 +199,7 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
   // two register sets for the input rows: a row is requested two steps before
   // it is used (HBM latency under load exceeds a step)
   vu32x4 inr[2][K::IREG] = {};
-  const int nres = is_c ? PT : 0;                               // residual loads per step
+  const int nres = PT;                                          // residual loads per step
   const int nst = ((VOX_DBG(q) & 256) && blockIdx.x == 0) ? 1 : 0;  // trace stamps (stores)
   // The row loop's stores are inline asm and its waits counted by hand
   // (device_common.h vst16 / vm_wait): compiler-placed waits fell back to
@@ -233,8 +233,11 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
   // the residual row is requested one step ahead (a second register set would
   // push the chain's fragment reads onto the registers they are consumed from)
   vu32x4 resb[PT] = {};
-  auto load_res = [&](int r) __attribute__((always_inline)) {
-    if (!is_c) return;
+  // addresses of residual row r, formed while the previous row's values are
+  // still live: the register allocator then has no reason to build them in
+  // resb's registers, and the loads land in resb's registers directly (no
+  // copy -- a copy would wait for the loads at once, vld16)
+  auto res_addr = [&](int r, const void* (&ra)[PT]) __attribute__((always_inline)) {
 #pragma unroll
     for (int j = 0; j < PT; ++j) {
       const int px = 16 * j + col;
@@ -242,8 +245,19 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
       // the (CI = 32)-channel input row, for the shortcut MFMAs
       const int cho = K::PROJ ? 8 * g : 32 * pq + 8 * g;
       const bool ok = r >= h0 && r < h1 && px < W;
-      vld16(resb[j], ok ? (const void*)(X + (img + (size_t)r * W + px) * CI + cho) : zline);
+      ra[j] = ok ? (const void*)(X + (img + (size_t)r * W + px) * CI + cho) : (const void*)zline;
     }
+  };
+  // issued by every wave (the others read the zero line): one definition of
+  // resb on every path, so no merge copy of in-flight values at the join
+  auto load_res_at = [&](const void* const (&ra)[PT]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < PT; ++j) vld16(resb[j], is_c ? ra[j] : (const void*)zline);
+  };
+  auto load_res = [&](int r) __attribute__((always_inline)) {
+    const void* ra[PT];
+    res_addr(r, ra);
+    load_res_at(ra);
   };
 
   const int a0 = h0 - (S - 1);
@@ -280,6 +294,8 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
     auto& res = resb;
     const bool cstep = is_c && c >= h0 && c < h1 && !(VOX_DBG(q) & 2);
     const int ns_cur = cstep ? PT : 0;
+    const void* rnext[PT];
+    res_addr(c + 1, rnext);
     stamp(t, 0);
     // ---------------- phase 0: 1x1a (row a) | 1x1c (row c)
     if (is_a && !(VOX_DBG(q) & 1)) {
@@ -417,7 +433,7 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
 #pragma unroll
       for (int j = 0; j < PT; ++j) vm_launder(res[j]);
     }
-    if (!(VOX_DBG(q) & 8)) load_res(c + 1);
+    if (!(VOX_DBG(q) & 8)) load_res_at(rnext);
     stamp(t, 1);
     __syncthreads();
     stamp(t, 2);
