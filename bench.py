@@ -39,7 +39,7 @@ def _kernel_name(tag, dt):
             if tag & (1 << 17):
                 return "conv3x3_utt"
             return "conv3x3_s2r" if tag & (1 << 19) else "conv3x3_rw"
-        return "conv3x3_win" if tag & (1 << 19) else "conv3x3_pipe"
+        return "conv3x3_pipe"
     if tag & (1 << 28):
         return "gconv3x3_rows"
     if tag & (1 << 27):
@@ -55,7 +55,7 @@ def _kernel_name(tag, dt):
     if tag & (1 << 22):
         return f"split_chain<{(tag >> 4) & 15}, {(tag >> 8) & 15}>"
     if tag & (1 << 21):
-        return "gemm1x1_lds"
+        return "conv1x1_nw" if tag & (1 << 19) else "gemm1x1_lds"
     if tag & (1 << 20):
         return f"conv1x1_rr<{(tag >> 16) & 15}, {(tag >> 8) & 15}, {(tag >> 4) & 15}>"
     if tag & (1 << 15):

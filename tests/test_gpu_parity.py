@@ -344,6 +344,26 @@ def test_gemm_pipe_prologue_bitwise(weights, F, T, N, monkeypatch):
     assert np.array_equal(got, ref)
 
 
+@pytest.mark.parametrize("F,T,N", [(80, 64, 2), (40, 97, 3), (80, 33, 5)])
+def test_conv1x1_nw_bitwise_rr(weights, F, T, N, monkeypatch):
+    """DPN68's narrow 1x1s (K <= 256, <= 192 couts) on the LDS-resident-weight
+    GEMM (prologue in registers, residual below ysplit, dense channels past it,
+    ragged last chunk) give the same bits as conv1x1_rr."""
+    import torch
+    from voxsrc2020_speaker_verification_amd import synth
+    spec, t, blob = weights("dpn68", F)
+    x = synth.make_features(N, T, F, seed=19)
+    with _extractor(blob, "bf16") as ex:
+        got = ex.run(x)
+        nw = [l for l in ex.describe(torch.from_numpy(x).cuda()) if l.startswith("nw ")]
+        assert len(nw) >= 6, nw
+    monkeypatch.setenv("VOXEMB_NO_NW", "1")
+    with _extractor(blob, "bf16") as ex:
+        ref = ex.run(x)
+        assert not any(l.startswith("nw ") for l in ex.describe(torch.from_numpy(x).cuda()))
+    assert np.array_equal(got, ref)
+
+
 def test_bneck_segments_bitwise(weights, monkeypatch):
     """Row segmentation of the fused bottleneck (N=1 -> many segments, warm-up
     rows recomputed) gives the same bits as one segment per utterance."""

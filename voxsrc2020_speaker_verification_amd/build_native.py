@@ -26,6 +26,7 @@ SOURCES = [
     ("conv3r.hip", ["-O3"]),
     ("conv3u.hip", ["-O3"]),
     ("conv3s.hip", ["-O3"]),
+    ("gemm_nw.hip", ["-O3"]),
     ("fbank.hip", ["-O3"]),
     ("api.cpp", ["-O2"]),
     ("kaldi_host.cpp", ["-O2", "-ffp-contract=off"]),

@@ -255,6 +255,7 @@ struct vox_model {
   int no_gemm_pro = 0;     // VOXEMB_NO_GEMM_PRO: prologue 1x1 convs off the LDS-DMA GEMMs
   int no_gemm_taps = 0;    // VOXEMB_NO_GEMM_TAPS: TDNN dilated convs off gemm1x1_ws
   int no_smallk = 0;       // VOXEMB_NO_SMALLK: DPN 10-channel 1x1s on the generic conv
+  int no_nw = 0;           // VOXEMB_NO_NW: narrow 1x1s on conv1x1_rr instead of conv1x1_nw
   int pro_min_cout = 192;  // VOXEMB_PRO_MIN_COUT: narrowest prologue 1x1 on gemm1x1_ws
   int gemm_var = 0;        // VOXEMB_GEMM_VAR: -1 = gemm1x1_wide instead of gemm1x1_ws
                            // (bitwise A/B); other values are diagnostics (VOX_DIAG builds)
@@ -292,6 +293,7 @@ static const PlanEnv kPlanEnv[] = {
     {"VOXEMB_NO_GEMM_PRO", &vox_model::no_gemm_pro},
     {"VOXEMB_NO_GEMM_TAPS", &vox_model::no_gemm_taps},
     {"VOXEMB_NO_SMALLK", &vox_model::no_smallk},
+    {"VOXEMB_NO_NW", &vox_model::no_nw},
     {"VOXEMB_PRO_MIN_COUT", &vox_model::pro_min_cout},
     {"VOXEMB_GEMM_VAR", &vox_model::gemm_var},
     {"VOXEMB_GEMM_MIN_K", &vox_model::gemm_min_k},
@@ -691,6 +693,8 @@ static void emit_conv(Builder& B, const ConvW& cw, Act x, const void* x2, int ld
       }
     }
   }
+  // narrow 1x1s (K <= 256, <= 192 couts): weights resident in LDS (gemm_nw.hip)
+  if (op.type == 8 && !B.m->no_nw && conv1x1_nw_ok(p)) op.type = 29;
   // bf16 1x1 with a BN+ReLU input prologue (DPN bn_relu_conv, >= 192 couts):
   // the wave-specialised GEMM applies it to its B fragments
   // (gemm1x1_ws<.., GS_PRO>; a padded K reads finite neighbouring channels
@@ -1519,6 +1523,7 @@ static hipError_t run_op(vox_model* m, const Op& op, hipStream_t s) {
     case 25: return launch_conv3_rw(op.cp, m->num_cu, s);
     case 26: return launch_conv3_utt(op.cp, m->num_cu, s);
     case 27: return launch_conv1x1_smallk(op.cp, s);
+    case 29: return launch_conv1x1_nw(op.cp, m->num_cu, s);
     case 28: return launch_conv3_s2r(op.cp, m->num_cu, s);
     case 15: return launch_convert_bf16(op.src, (float*)op.dst, op.count, s);
     case 16: return launch_att_bias_tanh((float*)op.dst, (const float*)op.src, op.N, op.H, op.W, op.C, s);
@@ -1755,6 +1760,8 @@ extern "C" int vox_profile(vox_model* m, const float* d_x, int n, int t, int f, 
         tag |= (1 << 23);
       else if (o.type == 27)
         tag |= (1 << 23) | (1 << 19);
+      else if (o.type == 29)
+        tag |= (1 << 21) | (1 << 19);
       else if (o.type == 12)
         tag |= (1 << 24);
       else if (o.type == 13)
@@ -1808,13 +1815,13 @@ extern "C" int vox_plan_describe(vox_model* m, const float* d_x, int n, int t, i
                              "win", "rr", "gemm", "chain", "stem", "bneck", "chainrows", "splits2",
                              "cvt16", "atttanh", "attpool", "gemmpipe", "gconv", "conv3pipe",
                              "gemmwide", "s2fused", "-", "chainfused", "conv3rw", "conv3utt",
-                             "smallk", "conv3s2r"};
+                             "smallk", "conv3s2r", "nw"};
   for (const Op& o : m->plan) {
     char line[256];
     const ConvParams& p = o.cp;
     if (o.type == 0 || o.type == 5 || o.type == 7 || o.type == 8 || o.type == 9 || o.type == 18 ||
         o.type == 20 || o.type == 21 || o.type == 25 || o.type == 26 ||
-        o.type == 27 || o.type == 28)
+        o.type == 27 || o.type == 28 || o.type == 29)
       std::snprintf(line, sizeof(line),
                     "%s wco=%d wpx=%d s=%d N=%d H=%d W=%d Cin=%d Ho=%d Wo=%d Cout=%d k=%dx%d st=%d "
                     "g=%d flags=%d x2=%d pro=%d flops=%.4g bytes=%.4g\n",

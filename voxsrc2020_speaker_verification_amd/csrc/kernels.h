@@ -149,6 +149,11 @@ hipError_t launch_conv3_utt(const ConvParams& p, int num_cu, hipStream_t s);
 // block at 40 -> 20 columns, output tiles of 3 rows with their input window
 // staged once in LDS.
 int conv3_s2r_ok(const ConvParams& p);
+// Narrow 1x1 GEMM with the weights resident in LDS (gemm_nw.hip): K <= 256,
+// Cout <= 192 (DPN68's bn_relu_conv 1x1s), prologue / residual / ysplit as
+// conv1x1_rr, persistent 8-wave workgroups streaming 64-pixel chunks.
+int conv1x1_nw_ok(const ConvParams& p);
+hipError_t launch_conv1x1_nw(const ConvParams& p, int num_cu, hipStream_t s);
 hipError_t launch_conv3_s2r(const ConvParams& p, int num_cu, hipStream_t s);
 // Wide-tile variant (gemm_wide.hip): 256 x BN tiles, BN = 256 (Cout % 256 == 0)
 // or 192 (Cout % 192 == 0, no residual), K % 32 == 0, K >= 96, no prologue.
