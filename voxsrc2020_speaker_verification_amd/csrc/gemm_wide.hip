@@ -28,6 +28,8 @@
 // gemm1x1_pipe / gemm1x1_lds.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include <cstdint>
 #include <type_traits>
 
@@ -619,7 +621,7 @@ __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
       if (!RES && c_k == KT - 1) {
         epi(std::integral_constant<int, 0>{}, co0, px0, nullptr);
         epi(std::integral_constant<int, 1>{}, co0, px0, nullptr);
-        epi(std::integral_constant<int, 2>{}, co0, px0, nullptr);
+        if constexpr (NJ > 2) epi(std::integral_constant<int, 2>{}, co0, px0, nullptr);
         if constexpr (NJ > 3) epi(std::integral_constant<int, 3>{}, co0, px0, nullptr);
       }
     } else if (c_k < KT) {
@@ -655,15 +657,18 @@ __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
       if (!RES && c_k == KT - 1) {
         epi(std::integral_constant<int, 0>{}, co0, px0, nullptr);
         epi(std::integral_constant<int, 1>{}, co0, px0, nullptr);
-        epi(std::integral_constant<int, 2>{}, co0, px0, nullptr);
+        if constexpr (NJ > 2) epi(std::integral_constant<int, 2>{}, co0, px0, nullptr);
         if constexpr (NJ > 3) epi(std::integral_constant<int, 3>{}, co0, px0, nullptr);
       }
     } else if (RES) {
       const int ph = c_k - KT;
       if (ph == 0) epi(std::integral_constant<int, 0>{}, co0, px0, L);
       else if (ph == 1) epi(std::integral_constant<int, 1>{}, co0, px0, L);
-      else if (ph == 2) epi(std::integral_constant<int, 2>{}, co0, px0, L);
-      else if constexpr (NJ > 3) epi(std::integral_constant<int, 3>{}, co0, px0, L);
+      else if (ph == 2) {
+        if constexpr (NJ > 2) epi(std::integral_constant<int, 2>{}, co0, px0, L);
+      } else {
+        if constexpr (NJ > 3) epi(std::integral_constant<int, 3>{}, co0, px0, L);
+      }
     }
     if (c_k + 1 == SPT) {
 #pragma unroll
@@ -707,6 +712,18 @@ static void launch_wide_t(const ConvParams& p, int bn, int G, size_t lds, hipStr
     hipLaunchKernelGGL((gemm1x1_wide<256, false, DBG>), dim3(G), dim3(GW_NT), lds, s, p);
 }
 
+// pixels per tile: the default (192 for 256-wide tiles, 256 for 192-wide) or
+// 128 when the launch has too few tiles to fill the chip -- per tile the DMA
+// moves (BM + BN) rows per k-step, and ceil(tiles / CUs) rounds run in turn
+static int ws_bm(int M, int cblocks, int bn, int num_cu) {
+  const int big = bn == 256 ? 192 : 256;
+  auto cost = [&](int bm) {
+    const long t = (long)((M + bm - 1) / bm) * cblocks;
+    return ((t + num_cu - 1) / num_cu) * (long)(bm + bn);
+  };
+  return cost(128) < cost(big) ? 128 : big;
+}
+
 hipError_t launch_gemm_wide(const ConvParams& p0, int num_cu, int variant, hipStream_t s) {
   const int bn = gemm_wide_bn(p0);
   if (!bn) return hipErrorInvalidValue;
@@ -718,27 +735,33 @@ hipError_t launch_gemm_wide(const ConvParams& p0, int num_cu, int variant, hipSt
   int G = num_cu < T ? num_cu : T;
   G = G / 8 * 8;
   const size_t lds = GW_NST * GW_SLOT + 8 * (size_t)p.coutp + (p.in_mean ? 8 * (size_t)p.kp : 0);
+  const int bm = ws_bm(M, p.coutp / bn, bn, num_cu);
+  auto grid_for = [&](int bmx) {
+    const int t = ((M + bmx - 1) / bmx) * (p.coutp / bn);
+    int g = num_cu < t ? num_cu : t;
+    return g >= 8 ? g / 8 * 8 : g;
+  };
+  const int Gb = grid_for(bm);
   if (p.in_mean || p.kh > 1) {
     // operand variants (GS_PRO / GS_TAPS): wave-specialised only
-    const int T2 = ((M + 191) / 192) * (p.coutp / 256);
-    int G2 = num_cu < T2 ? num_cu : T2;
-    G2 = G2 >= 8 ? G2 / 8 * 8 : G2;
-    const int T3 = ((M + 255) / 256) * (p.coutp / 192);
-    int G3 = num_cu < T3 ? num_cu : T3;
-    G3 = G3 >= 8 ? G3 / 8 * 8 : G3;
+#define WS_L(BN_, RES_, BM_, MODE_) \
+  hipLaunchKernelGGL((gemm1x1_ws<BN_, RES_, BM_, 0, MODE_>), dim3(Gb), dim3(GS_NT), lds, s, p)
     if (p.in_mean) {
-      if (p.flags & EPI_RES)
-        hipLaunchKernelGGL((gemm1x1_ws<256, true, 192, 0, GS_PRO>), dim3(G2), dim3(GS_NT), lds, s, p);
-      else if (bn == 192)
-        hipLaunchKernelGGL((gemm1x1_ws<192, false, 256, 0, GS_PRO>), dim3(G3), dim3(GS_NT), lds, s, p);
-      else
-        hipLaunchKernelGGL((gemm1x1_ws<256, false, 192, 0, GS_PRO>), dim3(G2), dim3(GS_NT), lds, s, p);
+      if (p.flags & EPI_RES) {
+        if (bm == 128) WS_L(256, true, 128, GS_PRO); else WS_L(256, true, 192, GS_PRO);
+      } else if (bn == 192) {
+        if (bm == 128) WS_L(192, false, 128, GS_PRO); else WS_L(192, false, 256, GS_PRO);
+      } else {
+        if (bm == 128) WS_L(256, false, 128, GS_PRO); else WS_L(256, false, 192, GS_PRO);
+      }
     } else {
-      if (bn == 192)
-        hipLaunchKernelGGL((gemm1x1_ws<192, false, 256, 0, GS_TAPS>), dim3(G3), dim3(GS_NT), lds, s, p);
-      else
-        hipLaunchKernelGGL((gemm1x1_ws<256, false, 192, 0, GS_TAPS>), dim3(G2), dim3(GS_NT), lds, s, p);
+      if (bn == 192) {
+        if (bm == 128) WS_L(192, false, 128, GS_TAPS); else WS_L(192, false, 256, GS_TAPS);
+      } else {
+        if (bm == 128) WS_L(256, false, 128, GS_TAPS); else WS_L(256, false, 192, GS_TAPS);
+      }
     }
+#undef WS_L
     return hipGetLastError();
   }
   // wave-specialised by default (4-11 % faster per launch; the 256-wide tiles
@@ -749,17 +772,22 @@ hipError_t launch_gemm_wide(const ConvParams& p0, int num_cu, int variant, hipSt
   if (variant == 1 || (variant >= 21 && variant <= 29)) {   // wave-specialised
     auto go = [&](auto dbgc) {
       constexpr int D = decltype(dbgc)::value;
-      if (bn == 192) {
+      if (bm == 128) {
+        // too few tiles to fill the chip at the default size (small batches, TDNN)
+        if (bn == 192)
+          hipLaunchKernelGGL((gemm1x1_ws<192, false, 128, 0>), dim3(Gb), dim3(GS_NT), lds, s, p);
+        else if (p.flags & EPI_RES)
+          hipLaunchKernelGGL((gemm1x1_ws<256, true, 128, 0>), dim3(Gb), dim3(GS_NT), lds, s, p);
+        else
+          hipLaunchKernelGGL((gemm1x1_ws<256, false, 128, 0>), dim3(Gb), dim3(GS_NT), lds, s, p);
+      } else if (bn == 192) {
         hipLaunchKernelGGL((gemm1x1_ws<192, false, 256, D>), dim3(G), dim3(GS_NT), lds, s, p);
       } else {
         // 256-wide: 192-pixel tiles (their own tile count and grid)
-        const int T2 = ((M + 191) / 192) * (p.Cout / bn);
-        int G2 = num_cu < T2 ? num_cu : T2;
-        G2 = G2 >= 8 ? G2 / 8 * 8 : G2;
         if (p.flags & EPI_RES)
-          hipLaunchKernelGGL((gemm1x1_ws<256, true, 192, D>), dim3(G2), dim3(GS_NT), lds, s, p);
+          hipLaunchKernelGGL((gemm1x1_ws<256, true, 192, D>), dim3(Gb), dim3(GS_NT), lds, s, p);
         else
-          hipLaunchKernelGGL((gemm1x1_ws<256, false, 192, D>), dim3(G2), dim3(GS_NT), lds, s, p);
+          hipLaunchKernelGGL((gemm1x1_ws<256, false, 192, D>), dim3(Gb), dim3(GS_NT), lds, s, p);
       }
     };
 #ifdef VOX_DIAG
