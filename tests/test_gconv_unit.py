@@ -114,6 +114,9 @@ def run(N, H, W, Cc, gw, s, nseg, seed):
     (2, 21, 10, 1024, 32, 1, 2),   # stage 4 (RS 8, gw 32)
     (1, 41, 20, 1024, 32, 2, 2),   # stage 4 block 0
     (1, 5, 40, 128, 4, 1, 1),      # fewer rows than one window
+    (1, 7, 80, 128, 4, 1, 3),      # segments of 3, 3, 1 steps (the two-step prefetch's ends)
+    (2, 2, 80, 256, 8, 1, 1),      # a single step
+    (1, 9, 20, 512, 16, 1, 2),     # RS 4: a segment with one partial step
 ])
 def test_gconv_matches_emulation(N, H, W, Cc, gw, s, nseg):
     got, ref = run(N, H, W, Cc, gw, s, nseg, seed=H * 7 + gw)
