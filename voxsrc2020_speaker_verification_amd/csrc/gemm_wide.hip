@@ -387,7 +387,10 @@ __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
   constexpr int NLR = 32 / GS_NL;            // residual pieces per loader wave
   static_assert(GRP % GS_NL == 0, "groups per loader");
   static_assert(BN % 64 == 0, "weight pieces are the first BN/64 of a loader");
-  static_assert(!RES || BN == 256, "residual phases: 256 couts");
+  // residual phases carry 256 couts; the 320-wide tile (DPN68's 288-cout
+  // stage-3 1x1c, one cout block) takes its residual from those 256 only
+  // (the host checks ysplit <= 256 and a single cout block)
+  static_assert(!RES || BN == 256 || BN == 320, "residual phases: 256 couts");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -694,11 +697,15 @@ int gemm_wide_bn(const ConvParams& p) {
   int bn = 0;
   if (p.Cout % 256 == 0) bn = 256;
   else if (p.Cout % 192 == 0 && !(p.flags & EPI_RES)) bn = 192;
+  // DPN68 stage-3 1x1c: 256 residual couts + 32 dense ones in one 320-wide
+  // block (two 256-wide blocks re-read the activations for 32 couts)
+  else if (p.in_mean && p.Cout > 256 && p.Cout <= 320 && (!(p.flags & EPI_RES) || p.ysplit <= 256))
+    bn = 320;
   // DPN prologue convs: partial last cout tile (the weights hold 256-row multiples)
   else if (p.in_mean && p.Cout >= 128) bn = 256;
   if (!bn || p.Cout > 2048) return 0;
   if ((p.flags & EPI_RES) && (!p.res || p.ldr % 8)) return 0;
-  const int T = ((M + GW_BM - 1) / GW_BM) * (p.Cout / bn);
+  const int T = ((M + GW_BM - 1) / GW_BM) * ((p.Cout + bn - 1) / bn);
   return T >= 8 ? bn : 0;
 }
 
@@ -735,7 +742,8 @@ hipError_t launch_gemm_wide(const ConvParams& p0, int num_cu, int variant, hipSt
   int G = num_cu < T ? num_cu : T;
   G = G / 8 * 8;
   const size_t lds = GW_NST * GW_SLOT + 8 * (size_t)p.coutp + (p.in_mean ? 8 * (size_t)p.kp : 0);
-  const int bm = ws_bm(M, p.coutp / bn, bn, num_cu);
+  // (the 320-wide tile holds 80 accumulators per compute wave at 128 pixels)
+  const int bm = bn == 320 ? 128 : ws_bm(M, p.coutp / bn, bn, num_cu);
   auto grid_for = [&](int bmx) {
     const int t = ((M + bmx - 1) / bmx) * (p.coutp / bn);
     int g = num_cu < t ? num_cu : t;
@@ -747,7 +755,9 @@ hipError_t launch_gemm_wide(const ConvParams& p0, int num_cu, int variant, hipSt
 #define WS_L(BN_, RES_, BM_, MODE_) \
   hipLaunchKernelGGL((gemm1x1_ws<BN_, RES_, BM_, 0, MODE_>), dim3(Gb), dim3(GS_NT), lds, s, p)
     if (p.in_mean) {
-      if (p.flags & EPI_RES) {
+      if (bn == 320) {
+        if (p.flags & EPI_RES) WS_L(320, true, 128, GS_PRO); else WS_L(320, false, 128, GS_PRO);
+      } else if (p.flags & EPI_RES) {
         if (bm == 128) WS_L(256, true, 128, GS_PRO); else WS_L(256, true, 192, GS_PRO);
       } else if (bn == 192) {
         if (bm == 128) WS_L(192, false, 128, GS_PRO); else WS_L(192, false, 256, GS_PRO);
