@@ -912,7 +912,11 @@ static void emit_head(Builder& B, const float* pooled, int n, float* out) {
   p.kh = 1; p.kw = 1; p.sh = p.sw = p.dh = p.dw = 1;
   p.cinp = hw.cinp; p.kchunk = kchunk; p.flags = EPI_PARTIAL; p.ysplit = 1 << 30;
   p.groups = 1; p.cblocks = gy;
-  op.cl.wco = hw.wco; op.cl.wpx = 1; op.cl.vec = 1; op.cl.splitk = S;
+  // 128 pixels per workgroup at large batches: each workgroup re-reads its
+  // weight slice once per pixel block (64-pixel blocks read 84 MB of weights
+  // for a 21 MB matrix at B = 256); the K partition, and so every utterance's
+  // bits, do not depend on it
+  op.cl.wco = hw.wco; op.cl.wpx = n >= 128 ? 2 : 1; op.cl.vec = 1; op.cl.splitk = S;
   op.flops = 2.0 * n * D * hw.cout;
   op.bytes = 4.0 * ((double)n * D + (double)D * hw.cout);
   op.cp.fast4 = 0;

@@ -1245,8 +1245,20 @@ __global__ __launch_bounds__(256) void splitk_reduce(const float* __restrict__ p
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= (int64_t)M * cout) return;
   const int pix = (int)(idx / cout), c = (int)(idx - (int64_t)pix * cout);
+  // fixed order z = 0, 1, ..., S-1; the slab loads of 8 consecutive z issued
+  // together (a load -> add chain per slab waited out S L2 round trips)
+  const float* src = partial + (size_t)pix * coutp + c;
+  const size_t zs = (size_t)M * coutp;
   float v = 0.f;
-  for (int z = 0; z < S; ++z) v += partial[((size_t)z * M + pix) * coutp + c];
+  int z = 0;
+  for (; z + 8 <= S; z += 8) {
+    float t[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) t[u] = src[(size_t)(z + u) * zs];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v += t[u];
+  }
+  for (; z < S; ++z) v += src[(size_t)z * zs];
   if (flags & EPI_PRE_RELU) v = fmaxf(v, 0.f);
   if (flags & EPI_AFFINE) v = (v - mean[c]) * inv[c];
   if (flags & EPI_RELU) v = fmaxf(v, 0.f);
@@ -1315,6 +1327,8 @@ __global__ __launch_bounds__(64 * TS) void stats_pool_k(const T* __restrict__ x,
         for (int e = 0; e < VN; ++e) s[e] += v[i][e];
       }
     }
+    // (unrolled: the loads of 4 rows issue together, the sums keep their order)
+#pragma unroll 4
     for (int h = ts + RM * TS; h < H; h += TS) {
       const T* q = base + (size_t)h * rowstride;
 #pragma unroll
@@ -1347,6 +1361,7 @@ __global__ __launch_bounds__(64 * TS) void stats_pool_k(const T* __restrict__ x,
         }
       }
     }
+#pragma unroll 4
     for (int h = ts + RM * TS; h < H; h += TS) {
       const T* q = base + (size_t)h * rowstride;
 #pragma unroll
