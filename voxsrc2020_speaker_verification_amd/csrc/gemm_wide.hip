@@ -366,9 +366,10 @@ constexpr int GS_NL = 4;   // loader waves
 // reads and MFMAs (stores kept), 2 = loaders issue no DMA, 8 = loaders skip
 // the weight pieces (operand + residual DMA only); results garbage
 // MODE (operand variants; 0 = the Res2Net 1x1s):
-//   GS_PRO : BN + ReLU prologue on the B fragments, relu((x - m[k]) * inv[k])
+//   GS_PRO : BN + ReLU prologue on the B operand, relu((x - m[k]) * inv[k])
 //            rounded to bf16, as gemm1x1_pipe<.., PRO> (DPN bn_relu_conv,
-//            dpn_model.py:40-45); channels k >= Cin of a padded K get m = inv = 0
+//            dpn_model.py:40-45), applied in LDS by the loader waves to the
+//            pieces they loaded; channels k >= Cin of a padded K get m = inv = 0
 //   GS_TAPS: 1-D dilated conv along H (W = 1, the TDNN layers,
 //            tdnn_model.py:24-30): K = taps x cinp, k-step -> (tap, channel
 //            chunk), B row of pixel (n, h) at tap t = input row h + t dh - ph of
@@ -488,8 +489,15 @@ __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
       }
     };
     // returns the pieces issued (an operand step NLL, a residual phase NLR)
+    // GS_PRO: the k-step each ring slot was filled with (16-bit fields, 0xFFFF =
+    // a residual phase), for the prologue pass below
+    uint64_t kinfo = ~0ull;
     auto issue = [&](int slot) -> int {
       int n = 0;
+      if constexpr (PRO) {
+        const uint64_t v = l_k < KT ? (uint64_t)l_k : 0xFFFFull;
+        kinfo = (kinfo & ~(0xFFFFull << (16 * slot))) | (v << (16 * slot));
+      }
       if (l_k < KT) {
         // GS_TAPS: this k-step's tap and channel chunk (wave-uniform)
         const int tap = TAPS ? (32 * l_k) / p.cinp : 0;
@@ -535,8 +543,40 @@ __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
     set_load_tile(0);
     issue(0);
     int n1 = issue(1), n2 = issue(2);   // pieces of the two steps after the awaited one
+    // GS_PRO: this lane's K chunk within a k-step (the DMA swizzle of an
+    // activation row depends only on the lane: row = 16 gi + lane / 4)
+    const int pc = (lane & 3) ^ ((4 - ((lane >> 4) & 3)) & 3);
     for (int s = 0; s < S; ++s) {
       gw_wait_vm(n1 + n2);   // step s landed; steps s+1, s+2 in flight
+      if constexpr (PRO) {
+        // the BN + ReLU prologue, applied once to the activation pieces this
+        // wave loaded, in LDS before the barrier: the compute waves read
+        // finished B fragments (each used to transform them itself, twice
+        // over -- both cout halves read the same fragment -- and that VALU
+        // work bound the DPN68 prologue GEMMs)
+        const int slot = s & 3;
+        const int ks = (int)((kinfo >> (16 * slot)) & 0xFFFFull);
+        if (ks != 0xFFFF) {
+          const int kb = 32 * ks + 8 * pc;
+          const f32x4 m0 = *reinterpret_cast<const f32x4*>(ptab + kb);
+          const f32x4 m1 = *reinterpret_cast<const f32x4*>(ptab + kb + 4);
+          const f32x4 i0 = *reinterpret_cast<const f32x4*>(ptab + p.kp + kb);
+          const f32x4 i1 = *reinterpret_cast<const f32x4*>(ptab + p.kp + kb + 4);
+#pragma unroll
+          for (int i = BN / 64; i < NLL; ++i) {
+            const int gi = lw + GS_NL * i;
+            bf16x8* q = reinterpret_cast<bf16x8*>(smem + slot * GW_SLOT + gi * 1024 + lane * 16);
+            bf16x8 b = *q;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              b[e] = (bf16_t)fmaxf(((float)b[e] - m0[e]) * i0[e], 0.f);
+              b[4 + e] = (bf16_t)fmaxf(((float)b[4 + e] - m1[e]) * i1[e], 0.f);
+            }
+            *q = b;
+          }
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+      }
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
       const int n3 = issue((s + 3) & 3);
@@ -632,22 +672,7 @@ __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
       bf16x8 a[NI], b[NJ];
 #pragma unroll
       for (int j = 0; j < NJ; ++j) b[j] = *reinterpret_cast<const bf16x8*>(L + offb + j * 1024);
-      if constexpr (PRO) {
-        // this lane's 8 K channels of the step: prologue on every B fragment
-        const int kb = 32 * c_k + 8 * g;
-        const f32x4 m0 = *reinterpret_cast<const f32x4*>(ptab + kb);
-        const f32x4 m1 = *reinterpret_cast<const f32x4*>(ptab + kb + 4);
-        const f32x4 i0 = *reinterpret_cast<const f32x4*>(ptab + p.kp + kb);
-        const f32x4 i1 = *reinterpret_cast<const f32x4*>(ptab + p.kp + kb + 4);
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            b[j][e] = (bf16_t)fmaxf(((float)b[j][e] - m0[e]) * i0[e], 0.f);
-            b[j][4 + e] = (bf16_t)fmaxf(((float)b[j][4 + e] - m1[e]) * i1[e], 0.f);
-          }
-        }
-      }
+      // (GS_PRO: the loader waves applied the prologue to these fragments)
       a[0] = *reinterpret_cast<const bf16x8*>(L + offa);
       a[1] = *reinterpret_cast<const bf16x8*>(L + offa + 1024);
 #pragma unroll
