@@ -5,7 +5,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/r3
+O=${O:-gpurun_out/r3}
 mkdir -p $O
 timeout -k 10 400 python3 bench.py > $O/bench.json 2> $O/bench.err || exit $?
 timeout -k 10 300 python3 bench.py --precision fp32 --steps 5 --warmup 2 --no-cpu-baseline > $O/bench_fp32.json 2> $O/bench_fp32.err || exit $?
