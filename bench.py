@@ -229,7 +229,12 @@ def main():
     x = torch.from_numpy(synth.make_features(B, T, F, seed=1000 + rank)).to(dev)
     out = torch.empty((B, ex.dim), dtype=torch.float32, device=dev)
     gathered = [torch.empty_like(out) for _ in range(world)] if world > 1 else None
-    stream = torch.cuda.current_stream(dev)
+    # a dedicated stream (the legacy default stream's handle 0 would make the
+    # wrapper fence every step with a side stream, extractor._ordered); the
+    # inputs above are complete before it is used
+    torch.cuda.synchronize(dev)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
 
     def step():
         ex.run_device(x, out, stream)

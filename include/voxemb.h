@@ -70,7 +70,10 @@ int vox_precision(const vox_model* m);
 
 /* x: host [n,t,f] float32 row-major; out: host [n, vox_dim] float32. */
 int vox_embed(vox_model* m, const float* x, int n, int t, int f, float* out);
-/* d_x, d_out: device pointers on the handle's device; stream may be NULL. */
+/* d_x, d_out: device pointers on the handle's device; stream may be NULL (the
+ * handle's own non-blocking stream -- NOT the HIP default stream: work the
+ * caller queued on the default stream is not ordered before it, so pass an
+ * explicit stream, or synchronise, when the inputs were produced there). */
 int vox_embed_device(vox_model* m, const float* d_x, int n, int t, int f,
                      float* d_out, void* stream);
 /* One utterance of any length t >= 25, chunked at 1000 frames. */

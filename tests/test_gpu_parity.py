@@ -511,6 +511,27 @@ def test_run_device_new_buffers_without_sync(weights):
         assert np.array_equal(g, r)
 
 
+def test_run_device_staged_reuses_plan(weights):
+    """run_device_staged (frontend.embed_wavs' path): same-shape batches go
+    through one pair of staged buffers, so the native plan keeps its pointers
+    and replays its graph; results equal the synchronous host path, also when
+    the staged output is overwritten by the next same-shape batch."""
+    import torch
+    from voxsrc2020_speaker_verification_amd import synth
+    spec, t, blob = weights("res2net50_w24_s4_c32", 80)
+    xs = [synth.make_features(4, 120, 80, seed=s) for s in (71, 72, 73)]
+    with _extractor(blob, "bf16") as ex:
+        got = []
+        for x in xs + [synth.make_features(3, 120, 80, seed=74), xs[1]]:
+            o = ex.run_device_staged(torch.from_numpy(x).cuda())
+            got.append(o.cpu().numpy())   # copied before the next call reuses it
+        assert len(ex._stage) == 2
+        ref = [ex.run(x) for x in xs] + [ex.run(synth.make_features(3, 120, 80, seed=74)),
+                                         ex.run(xs[1])]
+    for g, r in zip(got, ref):
+        assert np.array_equal(g, r)
+
+
 @pytest.mark.parametrize("name,F,T,N", [("dpn68", 80, 64, 2), ("dpn68", 40, 97, 3), ("dpn68", 80, 600, 2)])
 def test_gemm_ws_prologue_bitwise(weights, name, F, T, N, monkeypatch):
     """DPN68's BN+ReLU-prologue 1x1 convs (>= 192 couts) on gemm1x1_ws<.., GS_PRO>:

@@ -293,8 +293,8 @@ def embed_wavs(extractor, waves, opts=None, batch=64, cmn=True, keys=None, compr
     utts = [(str(i), feats[fo[i]:fo[i + 1]]) for i in range(len(waves))]
 
     def embed_batch(x):   # x: stacked device chunks [n, L, F]
-        out = torch.empty((x.shape[0], extractor.dim), dtype=torch.float32, device=dev)
-        extractor.run_device(x.contiguous(), out)
+        # staged buffers per shape: same-shape batches replay one captured graph
+        out = extractor.run_device_staged(x)
         torch.cuda.synchronize(dev)
         return out.cpu().numpy()
 
