@@ -128,13 +128,13 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
 #pragma unroll
   for (int k = 0; k < S - 1; ++k)
     for (int c = tid; c < 16 * WCO; c += NT) {
-      bmb[k * 16 * WCO + c] = c < WID ? q.mb[k][c] : 0.f;
+      bmb[k * 16 * WCO + c] = c < WID ? -q.mb[k][c] : 0.f;
       bib[k * 16 * WCO + c] = c < WID ? q.ib[k][c] : 0.f;
     }
-  for (int c = tid; c < K::SW; c += NT) { bma[c] = q.ma[c]; bia[c] = q.ia[c]; }
-  for (int c = tid; c < C; c += NT) { bmc[c] = q.mc[c]; bic[c] = q.ic[c]; }
+  for (int c = tid; c < K::SW; c += NT) { bma[c] = -q.ma[c]; bia[c] = q.ia[c]; }
+  for (int c = tid; c < C; c += NT) { bmc[c] = -q.mc[c]; bic[c] = q.ic[c]; }
   if (K::PROJ)
-    for (int c = tid; c < C; c += NT) { bmp[c] = q.mp[c]; bip[c] = q.ip[c]; }
+    for (int c = tid; c < C; c += NT) { bmp[c] = -q.mp[c]; bip[c] = q.ip[c]; }
 
   // ---- per-wave constant operands
   const bool is_a = wave < K::NPA;
@@ -312,11 +312,14 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
       const f32x4 i0 = *reinterpret_cast<const f32x4*>(bn1i);
       const f32x4 i1 = *reinterpret_cast<const f32x4*>(bn1i + 4);
       auto epi = [&](const f32x4& acc0, const f32x4& acc1, int px) __attribute__((always_inline)) {
+        // BN as (acc + (-mean)) * inv on packed fp32 pairs: x + (-m) == x - m
+        // exactly; the tables hold the negated means
+        const f32x4 t0 = (acc0 + m0) * i0, t1 = (acc1 + m1) * i1;
         bf16x8 o;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          o[e] = (bf16_t)((acc0[e] - m0[e]) * i0[e]);
-          o[4 + e] = (bf16_t)((acc1[e] - m1[e]) * i1[e]);
+          o[e] = (bf16_t)t0[e];
+          o[4 + e] = (bf16_t)t1[e];
         }
         o = relu_bf16(o);
         if (!inimg) o = bf16x8{};
@@ -375,23 +378,26 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
           // shortcut = bf16(bn_p(conv1x1_p(in))), as the unfused projection writes it
           const f32x4 z = {0.f, 0.f, 0.f, 0.f};
           const f32x4 s0 = mfma_step(wp[0], rv, z), s1 = mfma_step(wp[1], rv, z);
+          // (negated means in the table, as below)
           const f32x4 pm0 = *reinterpret_cast<const f32x4*>(bmp + ch);
           const f32x4 pm1 = *reinterpret_cast<const f32x4*>(bmp + ch + 4);
           const f32x4 pi0 = *reinterpret_cast<const f32x4*>(bip + ch);
           const f32x4 pi1 = *reinterpret_cast<const f32x4*>(bip + ch + 4);
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            rv[e] = (bf16_t)((s0[e] - pm0[e]) * pi0[e]);
-            rv[4 + e] = (bf16_t)((s1[e] - pm1[e]) * pi1[e]);
+            rv[e] = (bf16_t)((s0[e] + pm0[e]) * pi0[e]);
+            rv[4 + e] = (bf16_t)((s1[e] + pm1[e]) * pi1[e]);
           }
         }
+        // BN, then the residual add, each rounded like the unfused epilogue (no
+        // FMA); BN on packed pairs with the negated means of the table
+        const f32x4 t0 = (acc0 + m0) * i0, t1 = (acc1 + m1) * i1;
         bf16x8 o;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          // BN, then the residual add, each rounded like the unfused epilogue (no FMA)
 #pragma clang fp contract(off)
-          float v0 = (acc0[e] - m0[e]) * i0[e] + (float)rv[e];
-          float v1 = (acc1[e] - m1[e]) * i1[e] + (float)rv[4 + e];
+          float v0 = t0[e] + (float)rv[e];
+          float v1 = t1[e] + (float)rv[4 + e];
           o[e] = (bf16_t)v0;
           o[4 + e] = (bf16_t)v1;
         }
@@ -479,9 +485,10 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
       auto epilogue = [&](const f32x4& acc, int px) __attribute__((always_inline)) {
         if (!(co < WID && px < W)) return;
         const int pxo = px * ASTR + co * 2 + ASTR;
+        const f32x4 t = (acc + m) * sc;   // negated means in the table
         bf16x4 y;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) y[e] = (bf16_t)((acc[e] - m[e]) * sc[e]);
+        for (int e = 0; e < 4; ++e) y[e] = (bf16_t)t[e];
         y = relu_bf16(y);
         if (!inimg) y = bf16x4{};
         *reinterpret_cast<bf16x4*>(rings + ysl + pxo) = y;
@@ -626,7 +633,7 @@ __global__ __launch_bounds__((ChainRowsCfg<WID, S, PT>::NT)) void chain_rows(Cha
 #pragma unroll
   for (int k = 0; k < S - 1; ++k)
     for (int c = tid; c < 16 * WCO; c += NT) {
-      bmb[k * 16 * WCO + c] = c < WID ? q.mean[k][c] : 0.f;
+      bmb[k * 16 * WCO + c] = c < WID ? -q.mean[k][c] : 0.f;   // negated: BN as (x + (-m)) * inv
       bib[k * 16 * WCO + c] = c < WID ? q.inv[k][c] : 0.f;
     }
 
@@ -725,8 +732,11 @@ __global__ __launch_bounds__((ChainRowsCfg<WID, S, PT>::NT)) void chain_rows(Cha
         if (!(co < WID && px < W)) return;
         const int pxo = px * ASTR + co * 2 + ASTR;
         bf16x4 y;
+        {
+          const f32x4 t = (acc + m) * sc;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) y[e] = (bf16_t)((acc[e] - m[e]) * sc[e]);
+          for (int e = 0; e < 4; ++e) y[e] = (bf16_t)t[e];
+        }
         y = relu_bf16(y);
         if (emit)
           *reinterpret_cast<bf16x4*>(Bo + (img + (size_t)r * W + px) * q.ldb + (k - 1) * WID + co) = y;
@@ -844,11 +854,11 @@ __global__ __launch_bounds__((ChainFusedCfg<CI, WID, S, PT>::NT)) void chain_fus
 #pragma unroll
   for (int k = 0; k < S - 1; ++k)
     for (int c = tid; c < 16 * WCO; c += NT) {
-      bmb[k * 16 * WCO + c] = c < WID ? q.mean[k][c] : 0.f;
+      bmb[k * 16 * WCO + c] = c < WID ? -q.mean[k][c] : 0.f;   // negated: BN as (x + (-m)) * inv
       bib[k * 16 * WCO + c] = c < WID ? q.inv[k][c] : 0.f;
     }
   for (int c = tid; c < K::SW; c += NT) {
-    bma[c] = q.ma[c];
+    bma[c] = -q.ma[c];
     bia[c] = q.ia[c];
   }
   // tap table: for lane l and k-step s, the byte offset of its B fragment in
@@ -981,8 +991,11 @@ __global__ __launch_bounds__((ChainFusedCfg<CI, WID, S, PT>::NT)) void chain_fus
       for (int j = 0; j < PT; ++j) {
         const int px = 16 * j + col;
         bf16x4 o;
+        {
+          const f32x4 t = (acc[j] + m0) * i0;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = (bf16_t)((acc[j][e] - m0[e]) * i0[e]);
+          for (int e = 0; e < 4; ++e) o[e] = (bf16_t)t[e];
+        }
         o = relu_bf16(o);
         if (!inimg) o = bf16x4{};   // SAME padding rows of the chain
         if (px < W) {
@@ -1030,8 +1043,11 @@ __global__ __launch_bounds__((ChainFusedCfg<CI, WID, S, PT>::NT)) void chain_fus
         const int px = 16 * j + col;
         if (!(co < WID && px < W)) return;
         bf16x4 y;
+        {
+          const f32x4 t = (acc + m) * sc;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) y[e] = (bf16_t)((acc[e] - m[e]) * sc[e]);
+          for (int e = 0; e < 4; ++e) y[e] = (bf16_t)t[e];
+        }
         y = relu_bf16(y);
         if (emit)
           *reinterpret_cast<bf16x4*>(Bo + (img + (size_t)r * W + px) * q.ldb + (k - 1) * WID + co) = y;
@@ -1182,7 +1198,7 @@ __global__ __launch_bounds__((SplitS2Cfg<WID, S, WIN>::NT)) void split_s2_rows(C
 #pragma unroll
   for (int k = 0; k < S - 1; ++k)
     for (int c = tid; c < 16 * WCO; c += NT) {
-      bmb[k * 16 * WCO + c] = c < WID ? q.mean[k][c] : 0.f;
+      bmb[k * 16 * WCO + c] = c < WID ? -q.mean[k][c] : 0.f;   // negated: BN as (x + (-m)) * inv
       bib[k * 16 * WCO + c] = c < WID ? q.inv[k][c] : 0.f;
     }
 
@@ -1276,8 +1292,11 @@ __global__ __launch_bounds__((SplitS2Cfg<WID, S, WIN>::NT)) void split_s2_rows(C
       auto epilogue = [&](const f32x4& acc, int wo) __attribute__((always_inline)) {
         if (!(co < WID && wo < Wo)) return;
         bf16x4 y;
+        {
+          const f32x4 t = (acc + m) * sc;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) y[e] = (bf16_t)((acc[e] - m[e]) * sc[e]);
+          for (int e = 0; e < 4; ++e) y[e] = (bf16_t)t[e];
+        }
         y = relu_bf16(y);
         *reinterpret_cast<bf16x4*>(Bo + (imgo + (size_t)ho * Wo + wo) * q.ldb + ck * WID + co) = y;
       };
@@ -1422,11 +1441,11 @@ __global__ __launch_bounds__((S2FusedCfg<CI, WID, S, WIN>::NT)) void s2_fused(Ch
 #pragma unroll
   for (int k = 0; k < S - 1; ++k)
     for (int c = tid; c < 16 * WCO; c += NT) {
-      bmb[k * 16 * WCO + c] = c < WID ? q.mean[k][c] : 0.f;
+      bmb[k * 16 * WCO + c] = c < WID ? -q.mean[k][c] : 0.f;   // negated: BN as (x + (-m)) * inv
       bib[k * 16 * WCO + c] = c < WID ? q.inv[k][c] : 0.f;
     }
   for (int c = tid; c < K::SW; c += NT) {
-    bma[c] = q.ma[c];
+    bma[c] = -q.ma[c];
     bia[c] = q.ia[c];
   }
 
@@ -1552,8 +1571,11 @@ __global__ __launch_bounds__((S2FusedCfg<CI, WID, S, WIN>::NT)) void s2_fused(Ch
         char* dst = rings + p * PLANEB + ((r + 840) % 3) * ROWB + off * 2;
         const int px = 16 * j + col;
         bf16x4 o;
+        {
+          const f32x4 t = (a0 + m0) * i0;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = (bf16_t)((a0[e] - m0[e]) * i0[e]);
+          for (int e = 0; e < 4; ++e) o[e] = (bf16_t)t[e];
+        }
         o = relu_bf16(o);
         if (!inimg) o = bf16x4{};   // the fixed zero padding of the stride-2 convs
         if (px < W) *reinterpret_cast<bf16x4*>(dst + (px + 1) * ASTR) = o;
@@ -1616,8 +1638,11 @@ __global__ __launch_bounds__((S2FusedCfg<CI, WID, S, WIN>::NT)) void s2_fused(Ch
           const int wo = 16 * j + col;
           if (co < WID && wo < Wo) {
             bf16x4 y;
+            {
+              const f32x4 t = (acc[j] + m) * sc;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) y[e] = (bf16_t)((acc[j][e] - m[e]) * sc[e]);
+              for (int e = 0; e < 4; ++e) y[e] = (bf16_t)t[e];
+            }
             y = relu_bf16(y);
             *reinterpret_cast<bf16x4*>(Bo + (imgo + (size_t)ho * Wo + wo) * q.ldb + ck * WID + co) = y;
           }
