@@ -916,7 +916,7 @@ static void emit_head(Builder& B, const float* pooled, int n, float* out) {
   // weight slice once per pixel block (64-pixel blocks read 84 MB of weights
   // for a 21 MB matrix at B = 256); the K partition, and so every utterance's
   // bits, do not depend on it
-  op.cl.wco = hw.wco; op.cl.wpx = n >= 256 ? 4 : n >= 128 ? 2 : 1; op.cl.vec = 1; op.cl.splitk = S;
+  op.cl.wco = hw.wco; op.cl.wpx = n >= 128 ? 2 : 1; op.cl.vec = 1; op.cl.splitk = S;
   op.flops = 2.0 * n * D * hw.cout;
   op.bytes = 4.0 * ((double)n * D + (double)D * hw.cout);
   op.cp.fast4 = 0;
