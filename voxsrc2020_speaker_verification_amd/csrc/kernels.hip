@@ -1548,8 +1548,11 @@ static hipError_t stats_pool_ts(const T* x, int N, int H, int W, int C, const fl
     }
   }
   const unsigned blocks = (unsigned)((cols + 63) / 64);
-  // more time-slices when there are few columns or many frames
-  if (H >= 64 && blocks < 2048) {
+  // more time-slices for many frames.  The slice count fixes the summation
+  // order, so it depends on H only -- never on the batch (it used to drop to 4
+  // past 2,048 blocks, i.e. a TDNN utterance's pooled bits changed with the
+  // batch size past ~680 utterances)
+  if (H >= 64) {
     hipLaunchKernelGGL((stats_pool_k<T, VN, 8>), dim3(blocks), dim3(64 * 8), 0, s, x, N, H, W, C,
                        mean, inv, out);
   } else if (H >= 16) {
