@@ -126,17 +126,30 @@ def pmc_mfma_busy(summ):
     return {"conv_stack_mfma_busy": round(busy / cyc, 4) if cyc else None, "per_kernel": per}
 
 
-def weights_blob(model, feat_dim, cache_dir):
+def bench_weights(model, feat_dim):
+    """(spec, tensors, blob) of the benchmarked network: random-init weights of
+    the architecture, BN calibrated on synthetic features (seed 1).  The GPU
+    test of the headline plan (tests/test_bf16_oracle.py) uses the same."""
     from voxsrc2020_speaker_verification_amd import archs, synth, weights
-    path = os.path.join(cache_dir, f"voxemb_{model}_{feat_dim}_seed1.blob")
-    if os.path.exists(path):
-        with open(path, "rb") as f:
-            return f.read()
     spec = archs.get_arch(model, feat_dim)
     t = synth.make_weights(spec, seed=1)
     buf = io.BytesIO()
     weights.save_blob(buf, spec, t)
-    data = buf.getvalue()
+    return spec, t, buf.getvalue()
+
+
+def bench_features(batch, frames, feat_dim, rank=0):
+    """The synthetic FBANK batch rank `rank` extracts every step."""
+    from voxsrc2020_speaker_verification_amd import synth
+    return synth.make_features(batch, frames, feat_dim, seed=1000 + rank)
+
+
+def weights_blob(model, feat_dim, cache_dir):
+    path = os.path.join(cache_dir, f"voxemb_{model}_{feat_dim}_seed1.blob")
+    if os.path.exists(path):
+        with open(path, "rb") as f:
+            return f.read()
+    data = bench_weights(model, feat_dim)[2]
     try:
         os.makedirs(cache_dir, exist_ok=True)
         tmp = path + f".{os.getpid()}"
@@ -164,15 +177,20 @@ def _host_info():
 def cpu_baseline(model, feat_dim, T, blob, budget_s=15.0):
     """The C++/OpenMP fp32 restatement of the reference forward
     (oracle/cpu/voxcpu.cpp, the stand-in for tf_extract.py's TF1 CPU
-    `sess.run`; kind "port") on a bounded sample of the same workload, on the
-    host cores this job may use: OMP_NUM_THREADS when set (16 on the GPU boxes,
-    a one-GPU job's CPU share), else every core."""
+    `sess.run`; kind "port") on a bounded sample of the same workload, on
+    every host core this process may run on (its CPU affinity set,
+    SURVEY §8(d) "all host cores"); OMP_NUM_THREADS and nproc are recorded
+    beside it."""
     from oracle.cpu import CpuModel, build as cpu_build
     from voxsrc2020_speaker_verification_amd import synth
     cpu_build.build()
     m = CpuModel(blob)
     name, nproc = _host_info()
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or nproc
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = nproc
+    threads = affinity
     bs = 2 * threads
     x = synth.make_features(bs, T, feat_dim, seed=99)
     m.run(x[:2], threads)                       # workspace + weights warm
@@ -184,11 +202,16 @@ def cpu_baseline(model, feat_dim, T, blob, budget_s=15.0):
             break
     el = time.perf_counter() - t0
     avx512 = "avx512f" in open("/proc/cpuinfo").read() if os.path.exists("/proc/cpuinfo") else None
+    omp = os.environ.get("OMP_NUM_THREADS")
+    narrow = (f"; the process affinity allows {affinity} of the host's {nproc} cores"
+              if affinity < nproc else "")
     return {"value": round(n / el, 3), "unit": "utterances/sec", "cores": threads, "kind": "port",
-            "impl": "cpp_omp", "nproc": nproc, "cpu_model": name,
+            "impl": "cpp_omp", "nproc": nproc, "affinity_cores": affinity,
+            "omp_num_threads_env": omp, "cpu_model": name,
             "isa": "avx512" if avx512 else "avx2",
             "sample": f"{n} utterances of {T}x{feat_dim} in batches of {bs} ({el:.1f} s; "
-                      f"oracle/cpu/voxcpu.cpp fp32 C++/OpenMP, {threads} threads)"}
+                      f"oracle/cpu/voxcpu.cpp fp32 C++/OpenMP, {threads} threads = every core "
+                      f"in the process affinity set{narrow})"}
 
 
 def main():
@@ -212,23 +235,25 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    # under torchrun (WORLD_SIZE set) the RCCL path runs even at one rank: the
+    # per-step all-gather of the embeddings (cohort assembly) is in the timed region
+    dist_on = world > 1 or "WORLD_SIZE" in os.environ
+    if dist_on:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
-    dev = torch.device("cuda", local if world > 1 else 0)
+    dev = torch.device("cuda", local if dist_on else 0)
 
-    from voxsrc2020_speaker_verification_amd import synth
     from voxsrc2020_speaker_verification_amd.extractor import Extractor
 
     blob = weights_blob(args.model, args.feat_dim, args.cache_dir)
     ex = Extractor(blob, device=dev.index, precision=args.precision)
     B, T, F = args.batch, args.frames, args.feat_dim
-    x = torch.from_numpy(synth.make_features(B, T, F, seed=1000 + rank)).to(dev)
+    x = torch.from_numpy(bench_features(B, T, F, rank)).to(dev)
     out = torch.empty((B, ex.dim), dtype=torch.float32, device=dev)
-    gathered = [torch.empty_like(out) for _ in range(world)] if world > 1 else None
+    gathered = [torch.empty_like(out) for _ in range(world)] if dist_on else None
     # a dedicated stream (the legacy default stream's handle 0 would make the
     # wrapper fence every step with a side stream, extractor._ordered); the
     # inputs above are complete before it is used
@@ -238,23 +263,23 @@ def main():
 
     def step():
         ex.run_device(x, out, stream)
-        if world > 1:
+        if dist_on:
             dist.all_gather(gathered, out)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if dist_on:
         dist.barrier()
     el = time.perf_counter() - t0
-    if world > 1:
+    if dist_on:
         tt = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
@@ -347,13 +372,13 @@ def main():
                                             "calibrated weights)",
             "config": {"workload": f"{args.model} {F}x{T} extraction", "global_batch": B * world,
                        "per_gpu_batch": B, "frames": T, "feat_dim": F,
-                       "parallelism": f"dp{world}" + (" + RCCL all-gather" if world > 1 else "")},
+                       "parallelism": f"dp{world}" + (" + RCCL all-gather" if dist_on else "")},
             "roofline": roof,
             "cpu_baseline": cpu,
             **extra,
         }
         print(json.dumps(line))
-    if world > 1:
+    if dist_on:
         dist.barrier()
         dist.destroy_process_group()
     ex.close()

@@ -153,9 +153,9 @@ int vox_sliding_cmn_device(const float* d_in, const int64_t* d_frame_off, int n_
                            int cmn_window, int center, float* d_out, void* stream);
 /* Kaldi CompressedMatrix round trip of n_utt feature matrices [frames][f]
  * concatenated in d_in (`copy-feats --compress=true`, prepare_data.sh:69,
- * method kAutomaticMethod: "CM " kSpeechFeature for rows > 8, "CM2"
+ * method kAutomaticMethod: "CM " kSpeechFeature for rows > 8, "CM2 "
  * kTwoByteAuto otherwise).  Writes each utterance's compressed payload (the
- * bytes after the CM token, vox_cm_blob_bytes(rows, f) of them) at
+ * bytes after the "CM " / "CM2 " token, vox_cm_blob_bytes(rows, f) of them) at
  * d_blob + d_blob_off[u] (device int64[n_utt]) and, when d_out is non-NULL, the
  * decoded features as Kaldi's CopyToMat yields them (the matrix
  * apply-cmvn-sliding reads).  Asynchronous on `stream`.  n_utt <= 65535. */

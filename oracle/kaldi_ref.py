@@ -115,7 +115,8 @@ def cm_encode_kaldi(m):
     """Kaldi CompressedMatrix(mat, kAutomaticMethod) -> (token, payload bytes):
     "CM " (kSpeechFeature: per-column uint16 percentiles 0/25/75/100 at sorted
     positions 0, T/4, 3T/4, T-1 made strictly increasing, one byte per value,
-    column-major) for rows > 8, else "CM2" (kTwoByteAuto: uint16 row-major).
+    column-major) for rows > 8, else "CM2 " (kTwoByteAuto: uint16 row-major; Kaldi's
+    WriteToken ends every token with a space, so the CM2 token is 4 bytes).
     Global header: min, max of the matrix (a constant matrix gets
     max = min + (1 + |min|)), range = max - min."""
     f32 = np.float32
@@ -130,7 +131,7 @@ def cm_encode_kaldi(m):
     if rows <= 8:
         q = np.array([[_u16(mn, rng, m[i, j]) for j in range(cols)] for i in range(rows)],
                      np.uint16).reshape(rows, cols)
-        return b"CM2", head + q.tobytes()
+        return b"CM2 ", head + q.tobytes()   # WriteToken: "CM2" + " "
     c = f32(1.52590218966964e-05)
     hdrs, data = [], []
     q4 = rows // 4

@@ -136,3 +136,63 @@ def test_bf16_forward_tracks_bf16_oracle(weights, name, F, T, N):
     d_gpu, d_fp32 = rel(got, ref16), rel(ref32, ref16)
     print(f"{name}: mean rel L2 gpu-vs-bf16-oracle {d_gpu:.4f}, fp32-oracle-vs-bf16-oracle {d_fp32:.4f}")
     assert d_gpu < d_fp32
+
+
+def test_headline_plan_b256_matches_small_batches_and_oracle(monkeypatch):
+    """The exact plan bench.py times (BASELINE C3: res2net50_w24_s4_c32, 80x200,
+    B = 256, bf16, the bench's weights and rank-0 input; tf_extract.py:108).
+    * routing: the B = 256 plan runs the fused bottlenecks unsegmented
+      (nseg = 1) and the 1x1 GEMMs with the big tiles (192 pixels at 256 couts,
+      256 pixels at 192), unlike the small-batch plans below;
+    * rows [0:16] and [240:256] equal B = 16 runs of the same utterances bit for
+      bit, and the eager launch-by-launch run equals the captured graph;
+    * utterances 0 and 255 pass the per-layer bf16-oracle check above
+      (teacher-forced on their rows of every tap)."""
+    import re
+
+    import torch
+    import bench
+    from oracle import models_ref as R
+    from voxsrc2020_speaker_verification_amd.extractor import Extractor
+    name, F, T, B = "res2net50_w24_s4_c32", 80, 200, 256
+    spec, t, blob = bench.bench_weights(name, F)
+    x = bench.bench_features(B, T, F, rank=0)
+    xd = torch.from_numpy(x).cuda()
+    pick = [0, 255]
+    with Extractor(blob, device=0, precision="bf16") as ex:
+        desc = ex.describe(xd)
+        bn = [ln for ln in desc if ln.startswith("bneck ")]
+        assert len(bn) == 3 and all(" nseg=1 " in ln for ln in bn), bn
+        gw = [dict(re.findall(r"(\w+)=(\d+)", ln)) for ln in desc if ln.startswith("gemmwide ")]
+        assert len(gw) >= 20, desc
+        for g in gw:
+            assert (g["bn"], g["bm"]) in (("256", "192"), ("192", "256")), g
+        taps, emb = ex.layer_outputs(xd, utts=pick)
+        full = ex.run_device(xd)
+        torch.cuda.synchronize()
+        full = full.cpu().numpy()
+        lo, hi = ex.run(x[:16]), ex.run(x[B - 16:])
+        small = ex.describe(torch.from_numpy(x[:16]).cuda())
+    assert np.array_equal(emb, full)
+    assert np.array_equal(lo, full[:16]) and np.array_equal(hi, full[B - 16:])
+    assert any(" nseg=1 " not in ln for ln in small if ln.startswith("bneck "))  # a different plan
+    layers = R.layers(spec, t, "bf16")
+    assert len(taps) == len(layers) - 1
+    monkeypatch.setattr(R, "_ACC64", True)
+    prev, tot, tot_exact = x[pick], 0, 0.0
+    for (lname, f), got in zip(layers, taps + [emb[pick]]):
+        ref = f(prev)
+        assert got.shape == ref.shape, (lname, got.shape, ref.shape)
+        if lname == "pool+head":
+            err = float(np.abs(got - ref).max() / np.abs(ref).max())
+            assert err <= 1e-4, (lname, err)
+            break
+        st = compare_bf16(got, ref)
+        print(f"B=256 rows {pick} {lname}: exact {st['exact']:.5f} <=2ulp {st['le2']:.5f} bad {st['bad']:.2e}")
+        assert st["exact"] >= 0.94, (lname, st)
+        assert st["le2"] >= 0.99, (lname, st)
+        assert st["bad"] <= 1e-5, (lname, st)
+        tot += st["n"]
+        tot_exact += st["exact"] * st["n"]
+        prev = got
+    assert tot_exact / tot >= 0.99, tot_exact / tot

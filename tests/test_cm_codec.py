@@ -28,15 +28,15 @@ def _mats():
 def test_cm_encode_decodes_natively(i):
     m = list(_mats())[i]
     tok, pl = K.cm_encode_kaldi(m)
-    assert tok == (b"CM " if m.shape[0] > 8 else b"CM2")
+    assert tok == (b"CM " if m.shape[0] > 8 else b"CM2 ")
     got, used = kaldi.parse_mat(b"\0B" + tok + pl, cm="kaldi")
-    assert used == 5 + len(pl) and got.shape == m.shape
+    assert used == 2 + len(tok) + len(pl) and got.shape == m.shape
     ref = K.cm_decode_kaldi(pl) if tok == b"CM " else K.cm2_decode_kaldi(pl)
     assert np.array_equal(got, ref)
     # quantisation bound: the widest of the three piecewise-linear segments per
     # column (or one uint16 step for CM2) plus the header quantisation
     mn, rng = np.frombuffer(pl, np.float32, 2, 0)
-    if tok == b"CM2":
+    if tok == b"CM2 ":
         assert np.abs(got - m).max() <= rng / 65535 * 1.01
     else:
         cols = m.shape[1]
@@ -52,6 +52,6 @@ def test_cm2_rejected_by_kaldi_io_order():
     """kaldi_io's reader (kaldi_io.py:477) only accepts "CM "; so does ours in
     that mode, while cm="kaldi" reads CM2 as Kaldi C++ does."""
     tok, pl = K.cm_encode_kaldi(np.ones((3, 2), np.float32))
-    assert tok == b"CM2"
+    assert tok == b"CM2 "
     with pytest.raises(Exception):
         kaldi.parse_mat(b"\0B" + tok + pl, cm="kaldi_io")

@@ -135,3 +135,34 @@ def test_dp_extract_resume_skips_finished_shards(tmp_path):
     assert sorted(p.name for p in tmp_path.glob("ran*")) == ["ran2"]
     assert open(tmp_path / "xvector.ark", "rb").read() == first
     assert not list(tmp_path.glob("*.part*"))
+
+
+def test_atomic_writer_failure_publishes_nothing(tmp_path):
+    """A write that raises leaves neither the ark/scp pair nor .part files."""
+    from voxsrc2020_speaker_verification_amd.kaldi import VectorWriter
+    base = str(tmp_path / "xvector.1")
+    with pytest.raises(RuntimeError):
+        with VectorWriter(base, atomic=True) as w:
+            w.write("a", np.ones(4, np.float32))
+            raise RuntimeError("extractor died")
+    assert not list(tmp_path.iterdir())
+
+
+def test_resume_requires_matching_run_tag(tmp_path):
+    """--resume reuses a per-rank pair only if it was made with the same weights
+    and precision (the tag file beside it); otherwise the shard is recomputed."""
+    from voxsrc2020_speaker_verification_amd import dp_extract
+    from voxsrc2020_speaker_verification_amd.extract import write_vectors
+    blob = tmp_path / "m.blob"
+    blob.write_bytes(b"weights-1")
+    keys = ["u1", "u2"]
+    emb = np.arange(8, dtype=np.float32).reshape(2, 4)
+    base = str(tmp_path / "xvector")
+    write_vectors(base + ".1", keys, emb, atomic=True)
+    tag = dp_extract.run_tag(str(blob), "bf16")
+    assert dp_extract.completed_shard(base, 0, keys, 4, tag) is None      # no tag file yet
+    dp_extract._write_tag(base + ".1", tag)
+    assert np.array_equal(dp_extract.completed_shard(base, 0, keys, 4, tag), emb)
+    assert dp_extract.completed_shard(base, 0, keys, 4, dp_extract.run_tag(str(blob), "fp32")) is None
+    blob.write_bytes(b"weights-2")
+    assert dp_extract.completed_shard(base, 0, keys, 4, dp_extract.run_tag(str(blob), "bf16")) is None

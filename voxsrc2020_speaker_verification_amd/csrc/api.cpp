@@ -1497,8 +1497,20 @@ static int build_plan(vox_model* m, const float* x, int n, int t, float* out) {
   int rc = run(true);
   if (rc) return rc;
   // slack: kernels with a K padded to 32 (gemm1x1_ws prologue / taps) read up to
-  // 62 B past the last row of their input
-  for (int s = 0; s < S_NSLOTS; ++s) HIPCHK(m->slots[s].ensure(m->slot_need[s] + 4096));
+  // 62 B past the last row of their input.  Those bytes meet zero weights, but a
+  // NaN/Inf bit pattern times zero is still NaN in the MFMA, so a (re)allocated
+  // slot is zeroed once: afterwards every byte of it is zero or a value some
+  // kernel wrote (a smaller batch's input ends inside the slot, where the read
+  // past it lands on an earlier batch's finite data or on the zeros)
+  bool grew = false;
+  for (int s = 0; s < S_NSLOTS; ++s) {
+    const size_t want = m->slot_need[s] + 4096;
+    if (want <= m->slots[s].bytes) continue;
+    HIPCHK(m->slots[s].ensure(want));
+    HIPCHK(hipMemsetAsync(m->slots[s].p, 0, m->slots[s].bytes, m->stream));
+    grew = true;
+  }
+  if (grew) HIPCHK(hipStreamSynchronize(m->stream));
   rc = run(false);
   if (rc) return rc;
   m->plan_n = n;
@@ -1729,6 +1741,9 @@ extern "C" int vox_profile(vox_model* m, const float* d_x, int n, int t, int f, 
   std::vector<hipEvent_t> ev(nops + 1);
   for (auto& e : ev) HIPCHK(hipEventCreate(&e));
   std::vector<double> tot(nops, 0.0);
+  // the slots are shared with vox_embed_device launches on other streams:
+  // order after the previous one, and make the next one wait for this run
+  HIPCHK(hipStreamWaitEvent(s, m->done, 0));
   for (int r = 0; r < std::max(1, reps); ++r) {
     HIPCHK(hipEventRecord(ev[0], s));
     for (int i = 0; i < nops; ++i) {
@@ -1742,6 +1757,7 @@ extern "C" int vox_profile(vox_model* m, const float* d_x, int n, int t, int f, 
       tot[i] += ms;
     }
   }
+  HIPCHK(hipEventRecord(m->done, s));
   for (auto& e : ev) (void)hipEventDestroy(e);
   for (int i = 0; i < nops && i < max_ops; ++i) {
     if (op_ms) op_ms[i] = (float)(tot[i] / std::max(1, reps));
@@ -1859,6 +1875,12 @@ extern "C" int vox_plan_describe(vox_model* m, const float* d_x, int n, int t, i
     else
       std::snprintf(line, sizeof(line), "%s N=%d H=%d W=%d C=%d bytes=%.4g\n", tn[o.type], o.N,
                     o.H, o.W, o.C, o.bytes);
+    if (o.type == 21 && std::strlen(line) > 0) {   // + the tile (couts x pixels) it launches with
+      line[std::strlen(line) - 1] = 0;
+      char t[64];
+      std::snprintf(t, sizeof(t), " bn=%d bm=%d\n", gemm_wide_bn(p), gemm_wide_bm(p, m->num_cu));
+      std::strncat(line, t, sizeof(line) - std::strlen(line) - 1);
+    }
     out += line;
   }
   if (buf && cap > 0) {

@@ -234,7 +234,7 @@ __global__ void cmn_k(const float* __restrict__ in, const int64_t* __restrict__ 
 // ---- Kaldi CompressedMatrix round trip (`copy-feats --compress=true`,
 // prepare_data.sh:69; Kaldi compressed-matrix.cc, not vendored: its published
 // kAutomaticMethod -> kSpeechFeature for rows > 8, kTwoByteAuto otherwise).
-// Per utterance the blob is what follows the "CM " / "CM2" token:
+// Per utterance the blob is what follows the "CM " / "CM2 " token:
 //   float min, float range, int32 rows, int32 cols,
 //   rows > 8:  uint16 [cols][4] percentiles (0, 25, 75, 100), uint8 [cols][rows]
 //   rows <= 8: uint16 [rows][cols]

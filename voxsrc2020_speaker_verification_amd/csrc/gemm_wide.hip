@@ -756,6 +756,14 @@ static int ws_bm(int M, int cblocks, int bn, int num_cu) {
   return cost(128) < cost(big) ? 128 : big;
 }
 
+// pixels per tile launch_gemm_wide picks for this conv (plan descriptions, tests)
+int gemm_wide_bm(const ConvParams& p0, int num_cu) {
+  const int bn = gemm_wide_bn(p0);
+  if (!bn) return 0;
+  const int coutp = (p0.Cout + bn - 1) / bn * bn;
+  return bn == 320 ? 128 : ws_bm(p0.N * p0.Ho * p0.Wo, coutp / bn, bn, num_cu);
+}
+
 hipError_t launch_gemm_wide(const ConvParams& p0, int num_cu, int variant, hipStream_t s) {
   const int bn = gemm_wide_bn(p0);
   if (!bn) return hipErrorInvalidValue;

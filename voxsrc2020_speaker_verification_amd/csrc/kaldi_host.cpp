@@ -90,6 +90,10 @@ int parse_header(Reader& r, int* rows, int* cols, int* kind /*0 FM 1 DM 2 CM 3 C
   if (!r.take(h, 3)) return kfail(VOX_EIO, "truncated matrix header");
   if (h[0] == 'C' && h[1] == 'M') {
     if (h[2] != ' ' && h[2] != '2') return kfail(VOX_EIO, "CM3 compressed format is not supported");
+    if (h[2] == '2') {   // Kaldi WriteToken ends a token with a space: "CM2 "
+      char sp;
+      if (!r.take(&sp, 1) || sp != ' ') return kfail(VOX_EIO, "malformed CM2 token");
+    }
     float mn, range;
     int32_t nr, nc;
     if (!r.take(&mn, 4) || !r.take(&range, 4) || !r.take(&nr, 4) || !r.take(&nc, 4))

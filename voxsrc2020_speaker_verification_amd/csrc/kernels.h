@@ -159,6 +159,7 @@ hipError_t launch_conv3_s2r(const ConvParams& p, int num_cu, hipStream_t s);
 // or 192 (Cout % 192 == 0, no residual), K % 32 == 0, K >= 96, no prologue.
 // gemm_wide_bn returns BN or 0 when it does not apply.
 int gemm_wide_bn(const ConvParams& p);
+int gemm_wide_bm(const ConvParams& p, int num_cu);
 hipError_t launch_gemm_wide(const ConvParams& p, int num_cu, int variant, hipStream_t s);
 // Persistent LDS-DMA pipelined 3x3 implicit GEMM (conv3.hip) for the Res2Net
 // branch convs with Cin in {96, 192}: stride 1 (SAME) or 2 (fixed pad 1),

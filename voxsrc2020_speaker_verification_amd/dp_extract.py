@@ -61,15 +61,42 @@ def rank_failures(failed, device=None, group=None):
     return [r for r, f in enumerate(flags) if int(f.item())]
 
 
-def completed_shard(wspec, rank, keys, dim):
+def run_tag(weights_path, precision):
+    """What a shard's embeddings depend on besides its keys: the weight blob's
+    bytes and the precision.  Stored beside each per-rank pair
+    (`<wspec>.<i>.tag`) so --resume never reuses embeddings of another model."""
+    import hashlib
+    h = hashlib.sha256()
+    with open(weights_path, "rb") as f:
+        for blk in iter(lambda: f.read(1 << 22), b""):
+            h.update(blk)
+    return f"sha256={h.hexdigest()} precision={precision}"
+
+
+def _write_tag(base, tag):
+    tmp = f"{base}.tag.part{os.getpid()}"
+    with open(tmp, "w") as f:
+        f.write(tag + "\n")
+    os.replace(tmp, base + ".tag")
+
+
+def completed_shard(wspec, rank, keys, dim, tag=None):
     """The embeddings of rank's shard if `<wspec>.<rank+1>.ark/.scp` already
-    hold exactly `keys` (in order) as dim-D vectors, else None.  The pair is
-    written atomically (VectorWriter(atomic=True)), so a shard interrupted
-    mid-write is recomputed, never half-reused."""
+    hold exactly `keys` (in order) as dim-D vectors -- and, when `tag` is given,
+    were made by the same run tag (run_tag: weights + precision) -- else None.
+    The pair is written atomically (VectorWriter(atomic=True)), so a shard
+    interrupted mid-write is recomputed, never half-reused."""
     from .kaldi import read_vec_flt_ark
     base = f"{wspec}.{rank + 1}"
     if not (os.path.exists(base + ".ark") and os.path.exists(base + ".scp")):
         return None
+    if tag is not None:
+        try:
+            with open(base + ".tag") as f:
+                if f.read().strip() != tag:
+                    return None
+        except OSError:
+            return None
     try:
         with open(base + ".scp") as f:
             if [ln.split()[0] for ln in f if ln.strip()] != list(keys):
@@ -84,21 +111,24 @@ def completed_shard(wspec, rank, keys, dim):
 
 
 def run(rank, world, scp_items, embed_fn, dim, wspec, shard_file=None, batch=64,
-        device=None, write_per_rank=True, cohort_spk2utt=None, resume=False, shard_keys=None):
+        device=None, write_per_rank=True, cohort_spk2utt=None, resume=False, shard_keys=None,
+        tag=None):
     """The per-rank body (also used by the gloo tests with a fake embedder).
     scp_items: full list of (key, feat) is NOT required -- each rank only
     decodes its own shard: `scp_items` is a callable(rank, world) -> list of
     (key, [T,F] features).  resume: a rank whose per-rank ark/scp already hold
     its shard (`shard_keys(rank, world)` -> keys, without decoding features)
     reuses them -- the reference's per-shard processes are restartable one by
-    one in the same way (eval_inference_model.sh:29-36)."""
+    one in the same way (eval_inference_model.sh:29-36).  tag: the run tag
+    (run_tag) written beside each per-rank pair and required to match on
+    resume."""
     from .extract import embed_utterances, write_vectors
     err = None
     try:
         emb = None
         if resume and wspec and shard_keys is not None:
             keys = list(shard_keys(rank, world))
-            emb = completed_shard(wspec, rank, keys, dim)
+            emb = completed_shard(wspec, rank, keys, dim, tag)
         if emb is None:
             feats = scp_items(rank, world)
             emb = (embed_utterances(feats, embed_fn, dim, batch) if feats
@@ -106,7 +136,12 @@ def run(rank, world, scp_items, embed_fn, dim, wspec, shard_file=None, batch=64,
             keys = [k for k, _ in feats]
             if write_per_rank and wspec:
                 # xvector.<i>.ark as the reference; atomic for --resume
-                write_vectors(f"{wspec}.{rank + 1}", keys, emb, atomic=True)
+                base = f"{wspec}.{rank + 1}"
+                if tag is not None and os.path.exists(base + ".tag"):
+                    os.remove(base + ".tag")     # stale until the new pair is in place
+                write_vectors(base, keys, emb, atomic=True)
+                if tag is not None:
+                    _write_tag(base, tag)
     except Exception as e:   # e.g. ZeroDivisionError for a < 25-frame utterance
         err = e
     # every rank learns whether any shard failed BEFORE the gathers, so no rank
@@ -181,7 +216,7 @@ def main(argv=None):
     with Extractor(a.pb_file, device=local, precision=a.precision) as ex:
         run(rank, world, items, ex.run, ex.dim, a.wspec, batch=a.batch,
             device=torch.device("cuda", local), cohort_spk2utt=a.cohort_spk2utt,
-            resume=a.resume, shard_keys=keys)
+            resume=a.resume, shard_keys=keys, tag=run_tag(a.pb_file, a.precision))
     dist.barrier()
     dist.destroy_process_group()
     return 0

@@ -171,11 +171,13 @@ class Extractor:
         return buf.value.decode().strip().split("\n")
 
     # -- layer-by-layer parity support (tests) ------------------------------
-    def layer_outputs(self, x):
+    def layer_outputs(self, x, utts=None):
         """Run the plan for the device batch x ([N,T,F] float32 torch tensor)
         launch by launch and return (taps, embeddings): taps[i] is the output
         of oracle layer i (oracle/models_ref.py `layers`) as a float32 numpy
-        array [n,h,w,c], read right after the launch that completes it."""
+        array [n,h,w,c], read right after the launch that completes it.
+        utts: read only these utterances' rows of every tap ([len(utts),h,w,c];
+        the whole batch still runs -- for the big-batch plans)."""
         import torch
         n, t, f = x.shape
         out = torch.empty((n, self.dim), dtype=torch.float32, device=x.device)
@@ -191,14 +193,23 @@ class Extractor:
             check(L.vox_debug_run_ops(self._h, begin, tp.op_end, None))
             begin = tp.op_end
             es = 2 if tp.dtype == _native.VOX_BF16 else 4
-            rows = tp.n * tp.h * tp.w
-            raw = np.empty((rows, tp.ld * es), np.uint8)
-            check(L.vox_debug_read(raw.ctypes.data_as(C.c_void_p), C.c_void_p(tp.data), raw.nbytes))
+            sel = list(range(tp.n)) if utts is None else [int(u) for u in utts]
+            per = tp.h * tp.w * tp.ld * es          # bytes of one utterance's rows
+            raw = np.empty((len(sel), tp.h * tp.w, tp.ld * es), np.uint8)
+            if utts is None:
+                check(L.vox_debug_read(raw.ctypes.data_as(C.c_void_p), C.c_void_p(tp.data), raw.nbytes))
+            else:
+                for j, u in enumerate(sel):
+                    if not 0 <= u < tp.n:
+                        raise IndexError(f"utterance {u} outside the batch of {tp.n}")
+                    check(L.vox_debug_read(raw[j].ctypes.data_as(C.c_void_p),
+                                           C.c_void_p(tp.data + u * per), per))
+            raw = raw.reshape(len(sel) * tp.h * tp.w, tp.ld * es)
             if es == 2:
                 a = (raw.view(np.uint16)[:, :tp.c].astype(np.uint32) << 16).view(np.float32)
             else:
                 a = raw.view(np.float32)[:, :tp.c].copy()
-            res.append(a.reshape(tp.n, tp.h, tp.w, tp.c))
+            res.append(a.reshape(len(sel), tp.h, tp.w, tp.c))
         # the rest of the plan: pooling + head
         check(L.vox_debug_run_ops(self._h, begin, nops.value, None))
         return res, out.cpu().numpy()

@@ -221,7 +221,7 @@ def sliding_cmn_device(feats, frame_off, cmn_window=300, center=True, stream=Non
 
 
 def cm_blob_bytes(rows, cols):
-    """Bytes of a compressed payload after its "CM " (rows > 8) / "CM2" token."""
+    """Bytes of a compressed payload after its "CM " (rows > 8) / "CM2 " token."""
     return check(lib().vox_cm_blob_bytes(int(rows), int(cols)))
 
 
@@ -230,7 +230,7 @@ def cm_compress_device(feats, frame_off, stream=None, decode=True):
     device feature matrix: returns (decoded features [sum T, F] float32 on the
     device as Kaldi's CopyToMat yields them, or None; uint8 device blob; int64
     host blob offsets [n+1]).  Utterance u's payload is
-    blob[off[u]:off[u+1]], to follow b"CM " if it has > 8 frames else b"CM2"."""
+    blob[off[u]:off[u+1]], to follow b"CM " if it has > 8 frames else b"CM2 " (Kaldi tokens end in a space)."""
     import torch
     dev = feats.device
     fo = np.asarray(frame_off, np.int64)
@@ -263,7 +263,8 @@ def format_cm_record(key, payload, rows):
     k = key.encode("utf-8")
     if not k or b" " in k:
         raise ValueError("key must be non-empty without spaces")
-    return k + b" \0B" + (b"CM " if rows > 8 else b"CM2") + bytes(payload), len(k) + 1
+    # Kaldi WriteToken appends a space: "CM" -> b"CM ", "CM2" -> b"CM2 "
+    return k + b" \0B" + (b"CM " if rows > 8 else b"CM2 ") + bytes(payload), len(k) + 1
 
 
 def fbank(waves, opts=None, device=0, cmn=False, keys=None):

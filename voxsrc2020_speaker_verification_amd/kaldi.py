@@ -186,11 +186,28 @@ class VectorWriter:
                 os.replace(self.ark_path + self._sfx, self.ark_path)
                 os.replace(self.scp_path + self._sfx, self.scp_path)
 
+    def abort(self):
+        """Close without publishing: an atomic writer deletes its temporary
+        files, so a failed write never leaves a complete-looking pair."""
+        if self._ark:
+            self._ark.close()
+            self._scp.close()
+            self._ark = self._scp = None
+            if self._atomic:
+                for p in (self.ark_path + self._sfx, self.scp_path + self._sfx):
+                    try:
+                        os.remove(p)
+                    except OSError:
+                        pass
+
     def __enter__(self):
         return self
 
-    def __exit__(self, *a):
-        self.close()
+    def __exit__(self, exc_type, *a):
+        if exc_type is not None and self._atomic:
+            self.abort()
+        else:
+            self.close()
 
 
 def read_vec_flt_ark(path):
