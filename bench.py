@@ -38,6 +38,8 @@ def _kernel_name(tag, dt):
         if tag & (1 << 18):
             if tag & (1 << 17):
                 return "conv3x3_utt"
+            if tag & (1 << 16):
+                return "conv3x3_ks"
             return "conv3x3_s2r" if tag & (1 << 19) else "conv3x3_rw"
         return "conv3x3_pipe"
     if tag & (1 << 28):

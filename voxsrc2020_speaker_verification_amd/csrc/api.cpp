@@ -248,6 +248,7 @@ struct vox_model {
   int no_s2_fused = 0;     // VOXEMB_NO_S2_FUSED: 1x1a + split_s2_rows instead of s2_fused
   int no_chain_fused = 0;  // VOXEMB_NO_CHAIN_FUSED: 1x1a + chain_rows instead of chain_fused
   int no_conv3_rw = 0;     // VOXEMB_NO_CONV3_RW: conv3x3_pipe for the w = 96 stride-1 branches
+  int no_conv3_ks = 0;     // VOXEMB_NO_CONV3_KS: conv3x3_rw (not K-split) for them
   int no_conv3_utt = 0;    // VOXEMB_NO_CONV3_UTT: conv3x3_pipe for the w = 192 stride-1 branches
   int no_conv3_s2r = 0;    // VOXEMB_NO_CONV3_S2R: conv3x3_pipe for the w = 96 stride-2 branches
   int no_gconv = 0;        // VOXEMB_NO_GCONV: grouped 3x3 on the generic implicit GEMM
@@ -286,6 +287,7 @@ static const PlanEnv kPlanEnv[] = {
     {"VOXEMB_NO_S2_FUSED", &vox_model::no_s2_fused},
     {"VOXEMB_NO_CHAIN_FUSED", &vox_model::no_chain_fused},
     {"VOXEMB_NO_CONV3_RW", &vox_model::no_conv3_rw},
+    {"VOXEMB_NO_CONV3_KS", &vox_model::no_conv3_ks},
     {"VOXEMB_NO_CONV3_UTT", &vox_model::no_conv3_utt},
     {"VOXEMB_NO_CONV3_S2R", &vox_model::no_conv3_s2r},
     {"VOXEMB_NO_GCONV", &vox_model::no_gconv},
@@ -649,6 +651,10 @@ static void emit_conv(Builder& B, const ConvW& cw, Act x, const void* x2, int ld
   p.cinp = cw.cinp; p.kchunk = 0; p.flags = flags;
   p.groups = cw.groups;
   p.cblocks = cw.coutp / (16 * cw.wco);
+  // TDNN: one kernel route per layer whatever the batch (gemm1x1_ws even for a
+  // handful of tiles), so an utterance's embedding bits do not depend on its
+  // batch (tf_extract.py:27 extracts every utterance on its own)
+  p.any_m = B.m->family == "tdnn" ? 1 : 0;
   p.fast4 = (cw.cout % 4 == 0 && ldy % 4 == 0 && (ysplit >= (1 << 30) || (ysplit % 4 == 0 && ldy2 % 4 == 0)) &&
              (!res || ldr % 4 == 0) && cw.groups == 1) ? 1 : 0;
   op.cl.wco = cw.wco;
@@ -1308,8 +1314,10 @@ static int build_res2net(Builder& B, const float* x, int n, int t, float* out) {
           p.kh = br.kh; p.kw = br.kw; p.sh = p.sw = stride; p.dh = p.dw = 1; p.ph = p.pw = 1;
           p.groups = br.groups; p.flags = EPI_AFFINE | EPI_RELU;
           ok = br.wtc && br.mean && br.cin == w && br.cout == w && conv3_pipe_ok(p);
-          // stride-1 w = 96: weights in registers, window staged once per tile (conv3r.hip)
-          if (ok && !m->no_conv3_rw && conv3_rw_ok(p)) op.type = 25;
+          // stride-1 w = 96: K-split register weights, 32x32 MFMA tiles (conv3k.hip),
+          // or one 16-cout tile per wave (conv3r.hip, VOXEMB_NO_CONV3_KS)
+          if (ok && !m->no_conv3_ks && conv3_ks_ok(p)) op.type = 30;
+          else if (ok && !m->no_conv3_rw && conv3_rw_ok(p)) op.type = 25;
           // w = 192: one utterance band's window staged once, weights streamed (conv3u.hip)
           else if (ok && !m->no_conv3_utt && conv3_utt_ok(p)) op.type = 26;
           // stride 2, w = 96: register weights, 3-row window tiles (conv3s.hip)
@@ -1537,6 +1545,7 @@ static hipError_t run_op(vox_model* m, const Op& op, hipStream_t s) {
     case 22: return launch_s2_fused(op.ch, s);
     case 24: return launch_chain_fused(op.ch, s);
     case 25: return launch_conv3_rw(op.cp, m->num_cu, s);
+    case 30: return launch_conv3_ks(op.cp, m->num_cu, s);
     case 26: return launch_conv3_utt(op.cp, m->num_cu, s);
     case 27: return launch_conv1x1_smallk(op.cp, s);
     case 29: return launch_conv1x1_nw(op.cp, m->num_cu, s);
@@ -1804,6 +1813,8 @@ extern "C" int vox_profile(vox_model* m, const float* d_x, int n, int t, int f, 
         tag |= (1 << 29) | (1 << 18) | (1 << 17);
       else if (o.type == 28)
         tag |= (1 << 29) | (1 << 18) | (1 << 19);
+      else if (o.type == 30)
+        tag |= (1 << 29) | (1 << 18) | (1 << 16);
       else if (o.type == 8)
         tag |= (o.cl.wco << 4) | (o.cl.wpx << 8) | (((o.cp.cinp + 31) / 32) << 16) | (1 << 20);
       else if (o.type == 0 || o.type == 5)
@@ -1835,13 +1846,13 @@ extern "C" int vox_plan_describe(vox_model* m, const float* d_x, int n, int t, i
                              "win", "rr", "gemm", "chain", "stem", "bneck", "chainrows", "splits2",
                              "cvt16", "atttanh", "attpool", "gemmpipe", "gconv", "conv3pipe",
                              "gemmwide", "s2fused", "-", "chainfused", "conv3rw", "conv3utt",
-                             "smallk", "conv3s2r", "nw"};
+                             "smallk", "conv3s2r", "nw", "conv3ks"};
   for (const Op& o : m->plan) {
     char line[256];
     const ConvParams& p = o.cp;
     if (o.type == 0 || o.type == 5 || o.type == 7 || o.type == 8 || o.type == 9 || o.type == 18 ||
         o.type == 20 || o.type == 21 || o.type == 25 || o.type == 26 ||
-        o.type == 27 || o.type == 28 || o.type == 29)
+        o.type == 27 || o.type == 28 || o.type == 29 || o.type == 30)
       std::snprintf(line, sizeof(line),
                     "%s wco=%d wpx=%d s=%d N=%d H=%d W=%d Cin=%d Ho=%d Wo=%d Cout=%d k=%dx%d st=%d "
                     "g=%d flags=%d x2=%d pro=%d flops=%.4g bytes=%.4g\n",

@@ -252,7 +252,8 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
   // resb on every path, so no merge copy of in-flight values at the join
   auto load_res_at = [&](const void* const (&ra)[PT]) __attribute__((always_inline)) {
 #pragma unroll
-    for (int j = 0; j < PT; ++j) vld16(resb[j], is_c ? ra[j] : (const void*)zline);
+    for (int j = 0; j < PT; ++j)
+      vld16(resb[j], (is_c && !(VOX_DBG(q) & 512)) ? ra[j] : (const void*)zline);
   };
   auto load_res = [&](int r) __attribute__((always_inline)) {
     const void* ra[PT];

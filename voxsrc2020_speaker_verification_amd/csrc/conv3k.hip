@@ -1,0 +1,353 @@
+// K-split register-weight 3x3 conv for the w = 96 stride-1 Res2Net branches
+// (res2net_pad_conv_bn_relu, res2net_model.py:53-75, layer 3): y_k =
+// relu(bn(conv3x3(z_k))), and for k < S-1 the next branch's input
+// z_{k+1} = x_{k+1} + y_k formed in place over x_{k+1}.
+//
+// conv3x3_rw (conv3r.hip) holds one 16-cout tile's weights per wave and feeds
+// every v_mfma_f32_16x16x32_bf16 (16 cycles) a fresh 1-KB pixel fragment from
+// LDS: 12 waves x 108 fragments per 128-pixel tile = 1.3 MB of LDS reads, the
+// CU's whole LDS bandwidth at the MFMA rate, so the k-loop runs at the LDS
+// (with bank conflicts) rather than the matrix pipe.  Here every wave uses
+// v_mfma_f32_32x32x16_bf16 (32 cycles, 32 couts x 32 pixels x 16 k): the same
+// 1-KB pixel fragment now feeds twice the MFMA work, halving the LDS reads per
+// FLOP.  A 32-cout tile's full-K weights (216 VGPRs) do not fit the 12-wave
+// register budget, so K is split in halves:
+//
+//   wave = (cout group cg of 32, K half kh, pixel half ph): weights
+//   W[32 cg .. +32][432 kh .. +432] in 108 VGPRs; pixel groups 2 ph, 2 ph + 1
+//   (32 pixels each) of the 128-pixel tile, two accumulators of 16 VGPRs.
+//
+// After the k-loop the two K halves of a (cg, ph) pair meet in LDS: each wave
+// writes the partial sums of the pixel group its partner finishes (fp32, 4 KB)
+// and adds the partner's partial of its own group, so every output is
+// (half 0) + (half 1) in fp32 -- one fixed order, whatever wave finishes it.
+//
+// Window layout: pixel-major, 13 16-B units per pixel slot (12 chunks of 8
+// channels + 1 pad unit).  The odd 208-B pitch puts the 16 lanes of every
+// ds_read_b128 lane group (16 distinct consecutive slots of one chunk) on 16
+// disjoint 4-bank sets, and a window DMA piece reads 192 contiguous bytes per
+// pixel.  One zero slot between window rows serves as both rows' SAME padding
+// column (SW = W + 1).  Tiles are utterance-aligned (the padding is per
+// utterance); the window is double-buffered so the next tile's rows stream in
+// under this tile's MFMAs, and the y staging + deferred row-contiguous store
+// pass are conv3x3_rw's.
+// Not bitwise equal to conv3x3_pipe (K halves summed at the end, 16-deep MFMA
+// k-steps): the per-layer bf16 oracle check holds it (tests/test_bf16_oracle.py)
+// and tests/test_gpu_parity.py compares it with conv3x3_rw on the same input.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "device_common.h"
+#include "kernels.h"
+
+namespace vox {
+
+namespace {
+constexpr int KS_C = 96;               // Cin = Cout = branch width
+constexpr int KS_TP = 128;             // pixels per tile (4 groups of 32)
+constexpr int KS_NW = 12;              // 3 cout groups x 2 K halves x 2 pixel halves
+constexpr int KS_NT = 64 * KS_NW;
+constexpr int KS_SH = 9 * KS_C / 32;   // 27 k16-steps per K half (54 in all)
+constexpr int KS_NCH = KS_C / 8;       // 12 chunks per pixel
+constexpr int KS_PU = KS_NCH + 1;      // units per window slot (odd: conflict-free reads)
+constexpr int KS_PB = KS_PU * 16;      // 208 B
+constexpr int KS_XCH = KS_NW * 4096;   // partial-sum exchange: 4 KB per wave
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ void ks_glds16(const void* src, uint32_t lds) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(__builtin_amdgcn_readfirstlane(lds))
+      : "memory");
+}
+// the trailing s_nop keeps the next instruction from overwriting the data
+// registers before the store has read them
+__device__ __forceinline__ void ks_st16(void* dst, u32x4 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" : : "v"(dst), "v"(v) : "memory");
+}
+__device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+}  // namespace
+
+__device__ uint4 g_ks_zero[4] = {};
+__device__ uint4 g_ks_sink[64];   // destination of masked lanes' stores
+
+template <int W>
+struct KsCfg {
+  static constexpr int SW = W + 1;                                // slots per window row
+  static constexpr int RMAX = (W - 1 + KS_TP - 1) / W + 1 + 2;    // rows + halo a tile touches
+  static constexpr int SLOTS = RMAX * SW + 1;                     // + the last row's right pad
+  static constexpr int WPC = (SLOTS * KS_PU + 63) / 64;           // window DMA pieces
+  static constexpr int WBUF = WPC * 1024;
+  static constexpr int XZB = KS_TP * KS_C * 2;                    // x_{k+1} rows of a tile
+  static constexpr int XPC = XZB / 1024;
+  static constexpr int LDS = 2 * WBUF + KS_XCH + XZB + 2 * KS_C * 4;
+  static_assert(XZB % 1024 == 0, "x pieces");
+  static_assert(LDS <= 163840, "LDS");
+};
+
+#pragma clang fp contract(off)
+template <int W, bool HAS_Z>
+__global__ __launch_bounds__(KS_NT) void conv3x3_ks(ConvParams p) {
+  using K = KsCfg<W>;
+  constexpr int SW = K::SW;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r32 = lane & 31, h = lane >> 5;
+  const int cg = wave % 3, kh = (wave / 3) & 1, ph = wave / 6;
+  const int H = p.H, HW = p.H * W;
+  const int tpu = (HW + KS_TP - 1) / KS_TP;  // tiles per utterance
+  const int T = p.N * tpu;
+  int t_first, t_step, ntiles;
+  {
+    const int G = gridDim.x;
+    if ((G & 7) == 0) {
+      // XCD x (blocks x, x+8, ...) owns a contiguous tile range
+      const int x = blockIdx.x & 7, bi = blockIdx.x >> 3, nb = G >> 3;
+      const int b0 = (int)((long)x * T / 8), b1 = (int)((long)(x + 1) * T / 8);
+      t_first = b0 + bi;
+      t_step = nb;
+      ntiles = t_first < b1 ? (b1 - t_first + nb - 1) / nb : 0;
+    } else {
+      t_first = blockIdx.x;
+      t_step = G;
+      ntiles = t_first < T ? (T - t_first + G - 1) / G : 0;
+    }
+  }
+  if (ntiles == 0) return;
+
+  const bf16_t* __restrict__ X = reinterpret_cast<const bf16_t*>(p.x);
+  const bf16_t* __restrict__ XZ = reinterpret_cast<const bf16_t*>(p.res);
+  bf16_t* __restrict__ Y = reinterpret_cast<bf16_t*>(p.y);
+  bf16_t* __restrict__ Z = reinterpret_cast<bf16_t*>(p.y2);
+  const bf16_t* zero = reinterpret_cast<const bf16_t*>(g_ks_zero);
+  const uint32_t lds0 = (uint32_t)(uintptr_t)smem;
+  float* xch = reinterpret_cast<float*>(smem + 2 * K::WBUF);   // 4 KB per wave
+  char* xzb = smem + 2 * K::WBUF + KS_XCH;                      // x_{k+1} rows of the tile
+  float* bnm = reinterpret_cast<float*>(xzb + K::XZB);
+  float* bni = bnm + KS_C;
+  for (int c = tid; c < KS_C; c += KS_NT) {
+    bnm[c] = p.mean[c];
+    bni[c] = p.inv[c];
+  }
+
+  // A operand: cout row 32 cg + r32, k = 432 kh + 16 s + 8 h .. + 8
+  bf16x8 wr[KS_SH];
+  {
+    const bf16_t* __restrict__ Wt = reinterpret_cast<const bf16_t*>(p.w);
+    const bf16_t* wrow = Wt + (size_t)(32 * cg + r32) * (9 * KS_C) + 432 * kh + 8 * h;
+#pragma unroll
+    for (int s = 0; s < KS_SH; ++s) wr[s] = ld16(wrow + 16 * s);
+  }
+
+  // window piece q of tile tj into buffer b: units [64q, 64q + 64), unit u =
+  // chunk u % 13 of slot u / 13 (chunk 12 = the pad unit)
+  auto issue_win = [&](int tj, int b) __attribute__((always_inline)) {
+    const int id = t_first + tj * t_step;
+    const int n = id / tpu, t = id - n * tpu;
+    const int r0w = (t * KS_TP) / W - 1;   // image row of window row 0
+    for (int q = wave; q < K::WPC; q += KS_NW) {
+      int u = lane;
+      asm volatile("" : "+v"(u));
+      u += 64 * q;
+      const int x = u / KS_PU, c = u - x * KS_PU;
+      const int rr = x / SW, sc = x - rr * SW;
+      const int row = r0w + rr;
+      const bf16_t* src = zero;
+      if (c < KS_NCH && sc > 0 && rr < K::RMAX && row >= 0 && row < H)
+        src = X + ((size_t)n * HW + row * W + (sc - 1)) * p.ldx + c * 8;
+      ks_glds16(src, lds0 + (uint32_t)b * K::WBUF + (uint32_t)q * 1024u);
+    }
+  };
+
+  // the tile's x_{k+1} pixel rows (192 B each) into LDS, linear
+  auto issue_xz = [&](int tj) __attribute__((always_inline)) {
+    const int id = t_first + tj * t_step;
+    const int n = id / tpu, t = id - n * tpu;
+    const int p0 = t * KS_TP;
+#pragma unroll
+    for (int i = 0; i < (K::XPC + KS_NW - 1) / KS_NW; ++i) {
+      const int q = wave + KS_NW * i;
+      if (q < K::XPC) {
+        int u = lane;
+        asm volatile("" : "+v"(u));
+        u += 64 * q;
+        const int px = u / KS_NCH, c = u - px * KS_NCH;
+        const int pix = min(p0 + px, HW - 1);
+        ks_glds16(XZ + ((size_t)n * HW + pix) * p.ldr + c * 8,
+                  lds0 + 2u * K::WBUF + (uint32_t)KS_XCH + (uint32_t)q * 1024u);
+      }
+    }
+  };
+  // window pieces this wave issues per tile (wave-uniform)
+  const int nwin = (K::WPC - wave + KS_NW - 1) / KS_NW;
+
+  issue_win(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // this wave finishes pixel group 2 ph + kh of every tile and hands its
+  // partial of group 2 ph + (1 - kh) to its partner (cg, 1 - kh, ph)
+  const int gown = 2 * ph + kh, gpart = 2 * ph + (1 - kh);
+  const int partner = cg + 3 * (1 - kh) + 6 * ph;
+  for (int tj = 0; tj < ntiles; ++tj) {
+    const int b = tj & 1;
+    if (HAS_Z) issue_xz(tj);
+    if (tj + 1 < ntiles) issue_win(tj + 1, b ^ 1);
+    const int id = t_first + tj * t_step;
+    const int n = id / tpu, t = id - n * tpu;
+    const int p0 = t * KS_TP;
+    // lane-derived values re-formed per tile from a laundered lane id: kept
+    // live across the loop they cost the weights' registers (spills)
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const int r32 = ln & 31, h = ln >> 5;
+    // this lane's output pixel (group gown) and its 16-B cout chunks 16 i + 8 h
+    const int pxo = p0 + 32 * gown + r32;
+    const bool inpx = pxo < HW;
+    const size_t pix = (size_t)n * HW + (inpx ? pxo : HW - 1);
+    // byte address of the lane's pixel slot of group j shifted by (-1 row,
+    // -1 column), chunk h; + a compile-time tap/chunk offset per k16-step
+    auto base_of = [&](int j) __attribute__((always_inline)) {
+      const int pc = min(p0 + 32 * j + r32, HW - 1);
+      const int rr = pc / W - (p0 / W - 1);   // window row of the pixel (>= 1)
+      return b * K::WBUF + KS_PB * ((rr - 1) * SW + (pc % W)) + 16 * h;
+    };
+    // one pass: the 27 k16-steps of K half KH over pixel group j, one
+    // accumulation chain (32x32x16 needs no interleaving for throughput),
+    // fragments read two steps ahead
+    auto kpass = [&](auto khc, int j) __attribute__((always_inline)) {
+      constexpr int KH = decltype(khc)::value;
+      auto off = [](int s) constexpr {
+        const int S = 27 * KH + s, tap = S / 6, part = S % 6;
+        return KS_PB * ((tap / 3) * SW + tap % 3) + 32 * part;
+      };
+      const int bs = base_of(j);
+      f32x16 acc;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+      bf16x8 bf[3];
+      bf[0] = *reinterpret_cast<const bf16x8*>(smem + bs + off(0));
+      bf[1] = *reinterpret_cast<const bf16x8*>(smem + bs + off(1));
+#pragma unroll
+      for (int s = 0; s < KS_SH; ++s) {
+        if (s + 2 < KS_SH) {
+          bf[(s + 2) % 3] = *reinterpret_cast<const bf16x8*>(smem + bs + off(s + 2));
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        acc = mfma32(wr[s], bf[s % 3], acc);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      }
+      return acc;
+    };
+    f32x16 acc;
+    if (kh == 0) {
+      const f32x16 give = kpass(std::integral_constant<int, 0>{}, gpart);
+#pragma unroll
+      for (int r4 = 0; r4 < 4; ++r4)
+        *reinterpret_cast<f32x4*>(xch + wave * 1024 + r4 * 256 + ln * 4) =
+            f32x4{give[4 * r4], give[4 * r4 + 1], give[4 * r4 + 2], give[4 * r4 + 3]};
+      acc = kpass(std::integral_constant<int, 0>{}, gown);
+    } else {
+      const f32x16 give = kpass(std::integral_constant<int, 1>{}, gpart);
+#pragma unroll
+      for (int r4 = 0; r4 < 4; ++r4)
+        *reinterpret_cast<f32x4*>(xch + wave * 1024 + r4 * 256 + ln * 4) =
+            f32x4{give[4 * r4], give[4 * r4 + 1], give[4 * r4 + 2], give[4 * r4 + 3]};
+      acc = kpass(std::integral_constant<int, 1>{}, gown);
+    }
+    // this tile's x rows have landed: younger are the next window's pieces
+    if (HAS_Z) vm_wait(tj + 1 < ntiles ? nwin : 0);
+    __syncthreads();   // B: partials and x rows visible; every wave done with window b
+#pragma unroll
+    for (int r4 = 0; r4 < 4; ++r4) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(xch + partner * 1024 + r4 * 256 + ln * 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[4 * r4 + e] = acc[4 * r4 + e] + v[e];   // (half 0) + (half 1)
+    }
+    // y: register group q holds couts 32 cg + 8 q + 4 h + (0..3) of pixel pxo
+    unsigned yd[4][2];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int co = 32 * cg + 8 * q + 4 * h;
+      const f32x4 m = *reinterpret_cast<const f32x4*>(bnm + co);
+      const f32x4 iv = *reinterpret_cast<const f32x4*>(bni + co);
+      bf16x4 y;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) y[e] = (bf16_t)((acc[4 * q + e] - m[e]) * iv[e]);
+      y = relu_bf16(y);
+      const uint2 d = __builtin_bit_cast(uint2, y);
+      yd[q][0] = d.x;
+      yd[q][1] = d.y;
+    }
+    // lanes l and l + 32 (same pixel) hold couts 8q..8q+3 and 8q+4..8q+7: one
+    // half exchange per dword pair gives each lane 8 contiguous couts, chunk
+    // i = 16 i + 8 h (T21 of the HIP guide)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const auto r0 = __builtin_amdgcn_permlane32_swap(yd[2 * i][0], yd[2 * i + 1][0], false, false);
+      const auto r1 = __builtin_amdgcn_permlane32_swap(yd[2 * i][1], yd[2 * i + 1][1], false, false);
+      const u32x4 yc = {r0[0], r1[0], r0[1], r1[1]};
+      const size_t off = pix * p.ldy + 32 * cg + 16 * i + 8 * h;
+      // always issued (a masked pixel stores to a sink line) so every wave's
+      // vmcnt count below is the same
+      ks_st16(inpx ? (void*)(Y + off) : (void*)&g_ks_sink[ln], yc);
+      if (HAS_Z) {
+        const bf16x8 xb = *reinterpret_cast<const bf16x8*>(
+            xzb + (32 * gown + r32) * (KS_C * 2) + (32 * cg + 16 * i + 8 * h) * 2);
+        const bf16x8 yb = __builtin_bit_cast(bf16x8, yc);
+        bf16x8 zb;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) zb[e] = (bf16_t)((float)xb[e] + (float)yb[e]);
+        ks_st16(inpx ? (void*)(Z + pix * p.ldy2 + 32 * cg + 16 * i + 8 * h) : (void*)&g_ks_sink[ln],
+                __builtin_bit_cast(u32x4, zb));
+      }
+    }
+    // window tj+1 has landed: younger are only this tile's stores
+    if (HAS_Z) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    __syncthreads();   // D: next window visible; partials read before they are rewritten
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+int conv3_ks_ok(const ConvParams& p) {
+  if (p.Cin != KS_C || p.Cout != KS_C || p.kh != 3 || p.kw != 3 || p.groups != 1) return 0;
+  if (p.sh != 1 || p.sw != 1 || p.dh != 1 || p.dw != 1 || p.ph != 1 || p.pw != 1) return 0;
+  if (p.Ho != p.H || p.Wo != p.W || !(p.W == 20 || p.W == 10)) return 0;
+  if (p.kp != 9 * KS_C) return 0;   // weights [96][9 * 96], tap-major
+  if (p.ldx % 8 || p.ldy % 8 || p.ldr % 8 || p.ldy2 % 8) return 0;
+  if (p.flags != (EPI_AFFINE | EPI_RELU) || p.in_mean || p.x2 || !p.mean || !p.inv) return 0;
+  if (p.y2 && p.y2 != p.res) return 0;   // z_{k+1} in place over x_{k+1}
+  return p.N * p.H * p.W > 0;
+}
+
+hipError_t launch_conv3_ks(const ConvParams& p, int num_cu, hipStream_t s) {
+  if (!conv3_ks_ok(p)) return hipErrorInvalidValue;
+  const bool z = p.y2 != nullptr;
+  const int HW = p.H * p.W;
+  const int T = p.N * ((HW + KS_TP - 1) / KS_TP);
+  int G = num_cu < T ? num_cu : T;
+  if (G >= 8) G = G / 8 * 8;
+  if (p.W == 20) {
+    if (z) hipLaunchKernelGGL((conv3x3_ks<20, true>), dim3(G), dim3(KS_NT), KsCfg<20>::LDS, s, p);
+    else hipLaunchKernelGGL((conv3x3_ks<20, false>), dim3(G), dim3(KS_NT), KsCfg<20>::LDS, s, p);
+  } else {
+    if (z) hipLaunchKernelGGL((conv3x3_ks<10, true>), dim3(G), dim3(KS_NT), KsCfg<10>::LDS, s, p);
+    else hipLaunchKernelGGL((conv3x3_ks<10, false>), dim3(G), dim3(KS_NT), KsCfg<10>::LDS, s, p);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace vox

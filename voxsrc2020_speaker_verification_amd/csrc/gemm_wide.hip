@@ -731,7 +731,7 @@ int gemm_wide_bn(const ConvParams& p) {
   if (!bn || p.Cout > 2048) return 0;
   if ((p.flags & EPI_RES) && (!p.res || p.ldr % 8)) return 0;
   const int T = ((M + GW_BM - 1) / GW_BM) * ((p.Cout + bn - 1) / bn);
-  return T >= 8 ? bn : 0;
+  return (T >= 8 || p.any_m) ? bn : 0;
 }
 
 template <int DBG>
@@ -824,7 +824,7 @@ hipError_t launch_gemm_wide(const ConvParams& p0, int num_cu, int variant, hipSt
         else
           hipLaunchKernelGGL((gemm1x1_ws<256, false, 128, 0>), dim3(Gb), dim3(GS_NT), lds, s, p);
       } else if (bn == 192) {
-        hipLaunchKernelGGL((gemm1x1_ws<192, false, 256, D>), dim3(G), dim3(GS_NT), lds, s, p);
+        hipLaunchKernelGGL((gemm1x1_ws<192, false, 256, D>), dim3(Gb), dim3(GS_NT), lds, s, p);
       } else {
         // 256-wide: 192-pixel tiles (their own tile count and grid)
         if (p.flags & EPI_RES)

@@ -49,6 +49,9 @@ struct ConvParams {
   // gemm1x1_ws: paired-row bf16 weights re-blocked as [rows/16][kp/32][1 KB], each
   // 1-KB block one DMA piece in LDS order (swizzle applied), or null
   const void* wblk;
+  // gemm1x1_ws at any tile count (the plan fixes the route per model, not per
+  // batch: the TDNN's bits must not depend on how many utterances share a batch)
+  int any_m;
 };
 
 struct ConvLaunch {
@@ -142,6 +145,10 @@ hipError_t launch_gemm_pipe(const ConvParams& p, int num_cu, int variant, hipStr
 // registers, the input window staged once per 128-pixel tile.
 int conv3_rw_ok(const ConvParams& p);
 hipError_t launch_conv3_rw(const ConvParams& p, int num_cu, hipStream_t s);
+// K-split register-weight 3x3 (conv3k.hip): the same branches with 32x32x16
+// MFMA tiles, each wave holding half the K of a 32-cout group
+int conv3_ks_ok(const ConvParams& p);
+hipError_t launch_conv3_ks(const ConvParams& p, int num_cu, hipStream_t s);
 // Utterance-band window 3x3 conv for the w = 192 stride-1 branches (conv3u.hip)
 int conv3_utt_ok(const ConvParams& p);
 hipError_t launch_conv3_utt(const ConvParams& p, int num_cu, hipStream_t s);

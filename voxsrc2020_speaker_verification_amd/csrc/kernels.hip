@@ -13,6 +13,7 @@
 //                    res2net_model.py:240-241).
 //  * avgpool3s2   -- AvgPool 3x3/2 VALID over the fixed-padded tensor, divisor 9
 //                    (res2net_model.py:27-28,77).
+#include <cstdlib>
 #include "kernels.h"
 #include "device_common.h"
 
@@ -1535,6 +1536,14 @@ static hipError_t stats_pool_ts(const T* x, int N, int H, int W, int C, const fl
   const int64_t cols = (int64_t)N * W * (C / VN);
   if constexpr (sizeof(T) == 2 && VN == 8) {
     if (H <= 32) {
+#ifdef VOX_DIAG
+      static const int vn8 = [] { const char* e = std::getenv("VOXEMB_POOL_VN8"); return e ? std::atoi(e) : 0; }();
+      if (vn8 && H <= 25 && H > 16) {   // A/B: 8 channels (16-B loads) per thread
+        const unsigned b8 = (unsigned)((cols + 255) / 256);
+        hipLaunchKernelGGL((stats_pool_col<25, 8>), dim3(b8), dim3(256), 0, s, x, N, H, W, C, mean, inv, out);
+        return hipGetLastError();
+      }
+#endif
       // 4 channels (8 B) per thread: the rows of a column in 2 VGPRs each, so
       // the whole utterance axis is in flight at 8 waves per SIMD
       const unsigned b = (unsigned)((cols * 2 + 255) / 256);
