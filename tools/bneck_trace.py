@@ -39,4 +39,8 @@ for w in range(8):
     b1 = (t[w, :, 2] - t[w, :, 1]).mean()
     p1 = (t[w, :, 3] - t[w, :, 2]).mean()
     b2 = (t[w, 1:, 0] - t[w, :-1, 3]).mean()
-    print(f"wave {w}: phase0 {p0:7.0f}  wait1 {b1:7.0f}  phase1 {p1:7.0f}  wait2 {b2:7.0f}")
+    if int(os.environ.get("VOXEMB_BNECK_DBG", "0")) & 1024:
+        print(f"wave {w}: phase0 {p0:7.0f}  barrier1+staging {b1:7.0f}  chain MFMA loop {p1:7.0f}  "
+              f"epilogue+barrier2 {b2:7.0f}")
+    else:
+        print(f"wave {w}: phase0 {p0:7.0f}  wait1 {b1:7.0f}  phase1 {p1:7.0f}  wait2 {b2:7.0f}")

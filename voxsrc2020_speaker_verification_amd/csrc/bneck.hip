@@ -443,7 +443,9 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
     if (!(VOX_DBG(q) & 8)) load_res_at(rnext);
     stamp(t, 1);
     __syncthreads();
-    stamp(t, 2);
+    // (VOXEMB_BNECK_DBG bit 1024: stamps 2 and 3 after the input staging and
+    // after the chain's MFMA loop instead, to split phase 1)
+    if (!(VOX_DBG(q) & 1024)) stamp(t, 2);
     // ---------------- phase 1: all 3x3 stages, stage k on row a-2k+1
     if (!(VOX_DBG(q) & 8)) {
       // input row a+1 (loaded at step t-2): younger are step t-1's and this
@@ -452,6 +454,7 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
       store_in(P);
       load_in(P, a + 3);
     }
+    if (VOX_DBG(q) & 1024) stamp(t, 2);
     ns_prev = ns_cur;
     if (chain_wave && !(VOX_DBG(q) & 4)) {
       const int k = ck;
@@ -523,10 +526,13 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
         if (s + 1 < KST) __builtin_amdgcn_sched_group_barrier(0x008, PT, 0);   // then the MFMAs
         __builtin_amdgcn_sched_barrier(0);
       }
+      if (VOX_DBG(q) & 1024) stamp(t, 3);
 #pragma unroll
       for (int j = 0; j < PT; ++j) epilogue(acc[j], 16 * j + col);
+    } else if (VOX_DBG(q) & 1024) {
+      stamp(t, 3);
     }
-    stamp(t, 3);
+    if (!(VOX_DBG(q) & 1024)) stamp(t, 3);
     __syncthreads();
   };
   for (int t = 0; t < steps; t += 2) {
