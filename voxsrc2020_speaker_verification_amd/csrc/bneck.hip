@@ -139,6 +139,9 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
   // ---- per-wave constant operands
   const bool is_a = wave < K::NPA;
   const bool is_c = wave >= NW - K::NPC;
+  // (diagnostics: VOXEMB_BNECK_DBG 2048 = static priority 1 for the 1x1c waves,
+  // the longest phase-0 role)
+  if ((VOX_DBG(q) & 2048) && is_c) __builtin_amdgcn_s_setprio(1);
   const int pq = is_a ? wave : wave - (NW - K::NPC);   // 1x1 pair of this wave
   bf16x8 w1[K::KSW][2];
   {

@@ -450,6 +450,9 @@ __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
   }
   __syncthreads();
 
+  // (diagnostics: DBG 16 / 32 = static priority 1 for the loader / compute waves)
+  if ((DBG & 16) && loader) __builtin_amdgcn_s_setprio(1);
+  if ((DBG & 32) && !loader) __builtin_amdgcn_s_setprio(1);
   if (loader) {
     // ---- loader waves: groups gi = lw + 4 i of every step
     const bf16_t* src[NLL];
@@ -812,7 +815,7 @@ hipError_t launch_gemm_wide(const ConvParams& p0, int num_cu, int variant, hipSt
   // VOXEMB_GEMM_VAR=-1 selects gemm1x1_wide
   if (variant == 0) variant = 1;
   if (variant == -1) variant = 0;
-  if (variant == 1 || (variant >= 21 && variant <= 29)) {   // wave-specialised
+  if (variant == 1 || (variant >= 21 && variant <= 31)) {   // wave-specialised
     auto go = [&](auto dbgc) {
       constexpr int D = decltype(dbgc)::value;
       if (bm == 128) {
@@ -840,6 +843,8 @@ hipError_t launch_gemm_wide(const ConvParams& p0, int num_cu, int variant, hipSt
     else if (variant == 24) go(std::integral_constant<int, 4>{});
     else if (variant == 28) go(std::integral_constant<int, 8>{});
     else if (variant == 29) go(std::integral_constant<int, 9>{});
+    else if (variant == 30) go(std::integral_constant<int, 16>{});
+    else if (variant == 31) go(std::integral_constant<int, 32>{});
     else
 #endif
       go(std::integral_constant<int, 0>{});
