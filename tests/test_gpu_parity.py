@@ -377,6 +377,7 @@ def test_conv1x1_nw_bitwise_rr(weights, F, T, N, monkeypatch):
     from voxsrc2020_speaker_verification_amd import synth
     spec, t, blob = weights("dpn68", F)
     x = synth.make_features(N, T, F, seed=19)
+    monkeypatch.setenv("VOXEMB_NO_DPN_BLOCK", "1")   # stage 1's 1x1s unfused too
     with _extractor(blob, "bf16") as ex:
         got = ex.run(x)
         nw = [l for l in ex.describe(torch.from_numpy(x).cuda()) if l.startswith("nw ")]
@@ -385,6 +386,42 @@ def test_conv1x1_nw_bitwise_rr(weights, F, T, N, monkeypatch):
     with _extractor(blob, "bf16") as ex:
         ref = ex.run(x)
         assert not any(l.startswith("nw ") for l in ex.describe(torch.from_numpy(x).cuda()))
+    assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("T,N,nseg", [(64, 2, 0), (33, 5, 0), (600, 2, 0), (600, 2, 1), (97, 3, 7)])
+def test_dpn_block_bitwise_unfused(weights, T, N, nseg, monkeypatch):
+    """The fused stage-1 dual-path blocks (dpnblk.hip: 1x1a + grouped 3x3 + 1x1c
+    in one row-streamed launch, halo rows from the pre-pass, residual in place;
+    for the projection block the 3x3 + 1x1c after conv1x1_smallk's 1x1a) give
+    the same bits as the conv1x1_nw -> gconv3x3_rows -> conv1x1_nw launches,
+    every stage-1 tap and the embeddings, for any row segmentation (nseg 0 =
+    the plan's choice; 7 leaves a ragged last segment)."""
+    import torch
+    from voxsrc2020_speaker_verification_amd import synth
+    spec, t, blob = weights("dpn68", 80)
+    x = synth.make_features(N, T, 80, seed=23)
+    if nseg:
+        monkeypatch.setenv("VOXEMB_DPN_NSEG", str(nseg))
+    with _extractor(blob, "bf16") as ex:
+        xd = torch.from_numpy(x).cuda()
+        got = ex.run(x)
+        taps_got, _ = ex.layer_outputs(xd)
+        lines = [l for l in ex.describe(xd) if l.startswith("dpnblock")]
+        # stage 1: the projection block's 3x3 + 1x1c (1x1a on conv1x1_smallk), then
+        # two whole blocks
+        assert len(lines) == 3 and [("from_a=1" in l) for l in lines] == [True, False, False], lines
+        if nseg:
+            assert all(f"nseg={nseg}" in l for l in lines), lines
+    monkeypatch.delenv("VOXEMB_DPN_NSEG", raising=False)
+    monkeypatch.setenv("VOXEMB_NO_DPN_BLOCK", "1")
+    with _extractor(blob, "bf16") as ex:
+        xd = torch.from_numpy(x).cuda()
+        ref = ex.run(x)
+        taps_ref, _ = ex.layer_outputs(xd)
+        assert not any(l.startswith("dpnblock") for l in ex.describe(xd))
+    for i, (a, b) in enumerate(zip(taps_got, taps_ref)):
+        assert np.array_equal(a, b), f"tap {i}"
     assert np.array_equal(got, ref)
 
 

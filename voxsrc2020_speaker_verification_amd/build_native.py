@@ -25,6 +25,7 @@ SOURCES = [
     ("conv3.hip", ["-O3"]),
     ("conv3r.hip", ["-O3"]),
     ("conv3k.hip", ["-O3"]),
+    ("dpnblk.hip", ["-O3"]),
     ("conv3u.hip", ["-O3"]),
     ("conv3s.hip", ["-O3"]),
     ("gemm_nw.hip", ["-O3"]),

@@ -192,6 +192,7 @@ struct Op {
   ChainParams ch{};
   BneckParams bq{};  // type 12: Cin (cin), C, w (cl.wco), split (S)
   GconvParams gq{};  // type 19
+  DpnBlockParams dq{};  // type 31
   int cin = 0;
   double flops = 0, bytes = 0;
 };
@@ -257,6 +258,8 @@ struct vox_model {
   int no_gemm_taps = 0;    // VOXEMB_NO_GEMM_TAPS: TDNN dilated convs off gemm1x1_ws
   int no_smallk = 0;       // VOXEMB_NO_SMALLK: DPN 10-channel 1x1s on the generic conv
   int no_nw = 0;           // VOXEMB_NO_NW: narrow 1x1s on conv1x1_rr instead of conv1x1_nw
+  int no_dpn_block = 0;    // VOXEMB_NO_DPN_BLOCK: DPN stage-1 blocks as 1x1a / gconv / 1x1c launches
+  int dpn_nseg = 0;        // VOXEMB_DPN_NSEG: force dpn_block_rows' segments per utterance (tests)
   int pro_min_cout = 192;  // VOXEMB_PRO_MIN_COUT: narrowest prologue 1x1 on gemm1x1_ws
   int gemm_var = 0;        // VOXEMB_GEMM_VAR: -1 = gemm1x1_wide instead of gemm1x1_ws
                            // (bitwise A/B); other values are diagnostics (VOX_DIAG builds)
@@ -296,6 +299,8 @@ static const PlanEnv kPlanEnv[] = {
     {"VOXEMB_NO_GEMM_TAPS", &vox_model::no_gemm_taps},
     {"VOXEMB_NO_SMALLK", &vox_model::no_smallk},
     {"VOXEMB_NO_NW", &vox_model::no_nw},
+    {"VOXEMB_NO_DPN_BLOCK", &vox_model::no_dpn_block},
+    {"VOXEMB_DPN_NSEG", &vox_model::dpn_nseg},
     {"VOXEMB_PRO_MIN_COUT", &vox_model::pro_min_cout},
     {"VOXEMB_GEMM_VAR", &vox_model::gemm_var},
     {"VOXEMB_GEMM_MIN_K", &vox_model::gemm_min_k},
@@ -1418,47 +1423,110 @@ static int build_dpn(Builder& B, const float* x, int n, int t, float* out) {
         inp = Act{S, ctot, n, Ho, Wo, bw + dense};
       }
       const int Hi = inp.H, Wi = inp.W;
-      // 1x1a
       const BNW& b1 = m->bns[bi++];
       const ConvW& c1 = m->convs[ci++];
-      char* A = B.base(S_A, (size_t)n * Hi * Wi * r * es);
-      emit_conv(B, c1, inp, nullptr, 0, 1, 1, 1, 1, 0, 0, Hi, Wi, A, r, 0, nullptr, 0, nullptr, 0,
-                1 << 30, (const float*)b1.mean->p, (const float*)b1.inv->p);
-      // grouped 3x3, stride bs, TF SAME (asymmetric for stride 2)
       const BNW& b2 = m->bns[bi++];
       const ConvW& c2 = m->convs[ci++];
-      char* Bb = B.base(S_B, (size_t)n * Ho * Wo * r * es);
-      GconvParams g{};
-      g.x = A; g.ldx = r; g.in_mean = (const float*)b2.mean->p; g.in_inv = (const float*)b2.inv->p;
-      g.w = c2.wgc ? c2.wgc->p : nullptr; g.y = Bb; g.ldy = r;
-      g.N = n; g.H = Hi; g.W = Wi; g.C = r; g.Ho = Ho; g.Wo = Wo; g.gw = c2.cin;
-      g.sh = bs; g.ph = tf_same_beg(Hi, 3, bs); g.pw = tf_same_beg(Wi, 3, bs);
-      if (c2.wgc && !m->no_gconv && c2.cin * c2.groups == r && gconv_ok(g)) {
-        // row segments: enough workgroups to cover the chip a few times over,
-        // each segment >= 4 steps (warm-up window re-read per segment)
-        const int rs = gconv_rs(g);
-        int nseg = 1;
-        while ((long)n * (r / 64) * nseg < 2048 && Ho / (2 * nseg) >= 4 * rs) nseg *= 2;
-        g.seg = (Ho + nseg - 1) / nseg;
-        g.nseg = (Ho + g.seg - 1) / g.seg;
-        Op op;
-        op.kind = OP_CONV;
-        op.type = 19;
-        op.gq = g;
-        op.flops = 2.0 * n * Ho * Wo * (double)r * 9.0 * c2.cin;
-        op.bytes = es * ((double)n * Hi * Wi * r + (double)n * Ho * Wo * r);
-        B.ops->push_back(op);
-      } else {
-        emit_conv(B, c2, Act{A, r, n, Hi, Wi, r}, nullptr, 0, bs, bs, 1, 1, tf_same_beg(Hi, 3, bs),
-                  tf_same_beg(Wi, 3, bs), Ho, Wo, Bb, r, 0, nullptr, 0, nullptr, 0, 1 << 30,
-                  (const float*)b2.mean->p, (const float*)b2.inv->p);
-      }
-      // 1x1c -> [res add in place | new dense channels appended]
       const BNW& b3 = m->bns[bi++];
       const ConvW& c3 = m->convs[ci++];
-      emit_conv(B, c3, Act{Bb, r, n, Ho, Wo, r}, nullptr, 0, 1, 1, 1, 1, 0, 0, Ho, Wo, S, ctot,
-                EPI_RES, S, ctot, S ? S + (size_t)(bw + dense) * es : nullptr, ctot, bw,
-                (const float*)b3.mean->p, (const float*)b3.inv->p);
+      // stride-1 block at <= 80 columns and r = 128 (stage 1): 1x1a + grouped 3x3
+      // + 1x1c in one row-streamed launch (dpnblk.hip), bit-identical to the
+      // three launches below
+      // the grouped 3x3 + 1x1c part (and for b > 0 the 1x1a too) as one
+      // row-streamed launch (dpnblk.hip)
+      const bool rest_ok = bs == 1 && !m->no_dpn_block && m->dt == BF16 && c3.wpair && c2.wgc &&
+                           r == 128 && c2.cin <= 16 && c2.cin * c2.groups == r && c3.cin == r &&
+                           c3.cout == bw + inc && b2.mean && b3.mean;
+      auto block_params = [&](bool from_a, const void* xin) {
+        DpnBlockParams dq{};
+        dq.from_a = from_a ? 1 : 0;
+        dq.x = xin; dq.ldx = from_a ? r : ctot; dq.cin = from_a ? r : inp.C;
+        dq.res = S; dq.ldr = ctot;
+        if (!from_a) {
+          dq.w1 = c1.wpair->p; dq.kp1 = c1.kp;
+          dq.m1 = (const float*)b1.mean->p; dq.i1 = (const float*)b1.inv->p;
+        }
+        dq.wg = c2.wgc->p;
+        dq.m2 = (const float*)b2.mean->p; dq.i2 = (const float*)b2.inv->p;
+        dq.w3 = c3.wpair->p; dq.kp3 = c3.kp;
+        dq.m3 = (const float*)b3.mean->p; dq.i3 = (const float*)b3.inv->p;
+        dq.y = S; dq.y2 = S ? S + (size_t)(bw + dense) * es : nullptr; dq.ldy = ctot;
+        dq.bw = bw; dq.cout = c3.cout;
+        dq.N = n; dq.H = Ho; dq.W = Wo;
+        // one workgroup per CU (118 KB LDS): enough segments to cover the chip,
+        // each >= 8 rows (the first and last rows' 3x3 windows reach into the
+        // neighbours: their h1 rows are computed twice)
+        int nseg = m->dpn_nseg > 0 ? m->dpn_nseg : 1;
+        if (m->dpn_nseg <= 0)
+          while ((long)n * nseg < m->num_cu && Ho / (2 * nseg) >= 8) nseg *= 2;
+        dq.seg = (Ho + nseg - 1) / nseg;
+        dq.nseg = (Ho + dq.seg - 1) / dq.seg;
+        return dq;
+      };
+      auto push_block = [&](const DpnBlockParams& dq) {
+        Op op;
+        op.kind = OP_CONV;
+        op.type = 31;
+        op.dq = dq;
+        const double px = (double)n * Ho * Wo;
+        op.flops = 2.0 * px * (9.0 * r * c2.cin + (double)r * c3.cout);
+        op.bytes = es * px * ((double)bw + c3.cout + (dq.from_a ? r : inp.C));
+        if (!dq.from_a) op.flops += 2.0 * px * c1.cin * r;
+        B.ops->push_back(op);
+      };
+      DpnBlockParams dq{};
+      bool fused = false;
+      if (b > 0 && rest_ok && c1.wpair && c1.cout == r && c1.cin == inp.C && b1.mean) {
+        dq = block_params(false, S);
+        fused = dpn_block_ok(dq) != 0;
+        if (fused) dq.halo = B.base(S_A, dpn_block_halo_bytes(dq));
+      }
+      if (fused) {
+        push_block(dq);
+      } else {
+        // 1x1a
+        char* A = B.base(S_A, (size_t)n * Hi * Wi * r * es);
+        emit_conv(B, c1, inp, nullptr, 0, 1, 1, 1, 1, 0, 0, Hi, Wi, A, r, 0, nullptr, 0, nullptr, 0,
+                  1 << 30, (const float*)b1.mean->p, (const float*)b1.inv->p);
+        DpnBlockParams da = rest_ok ? block_params(true, A) : DpnBlockParams{};
+        if (rest_ok && dpn_block_ok(da)) {
+          push_block(da);
+          dense += inc;
+          B.tap(S, n, Ho, Wo, bw + dense, ctot);
+          continue;
+        }
+        // grouped 3x3, stride bs, TF SAME (asymmetric for stride 2)
+        char* Bb = B.base(S_B, (size_t)n * Ho * Wo * r * es);
+        GconvParams g{};
+        g.x = A; g.ldx = r; g.in_mean = (const float*)b2.mean->p; g.in_inv = (const float*)b2.inv->p;
+        g.w = c2.wgc ? c2.wgc->p : nullptr; g.y = Bb; g.ldy = r;
+        g.N = n; g.H = Hi; g.W = Wi; g.C = r; g.Ho = Ho; g.Wo = Wo; g.gw = c2.cin;
+        g.sh = bs; g.ph = tf_same_beg(Hi, 3, bs); g.pw = tf_same_beg(Wi, 3, bs);
+        if (c2.wgc && !m->no_gconv && c2.cin * c2.groups == r && gconv_ok(g)) {
+          // row segments: enough workgroups to cover the chip a few times over,
+          // each segment >= 4 steps (warm-up window re-read per segment)
+          const int rs = gconv_rs(g);
+          int nseg = 1;
+          while ((long)n * (r / 64) * nseg < 2048 && Ho / (2 * nseg) >= 4 * rs) nseg *= 2;
+          g.seg = (Ho + nseg - 1) / nseg;
+          g.nseg = (Ho + g.seg - 1) / g.seg;
+          Op op;
+          op.kind = OP_CONV;
+          op.type = 19;
+          op.gq = g;
+          op.flops = 2.0 * n * Ho * Wo * (double)r * 9.0 * c2.cin;
+          op.bytes = es * ((double)n * Hi * Wi * r + (double)n * Ho * Wo * r);
+          B.ops->push_back(op);
+        } else {
+          emit_conv(B, c2, Act{A, r, n, Hi, Wi, r}, nullptr, 0, bs, bs, 1, 1, tf_same_beg(Hi, 3, bs),
+                    tf_same_beg(Wi, 3, bs), Ho, Wo, Bb, r, 0, nullptr, 0, nullptr, 0, 1 << 30,
+                    (const float*)b2.mean->p, (const float*)b2.inv->p);
+        }
+        // 1x1c -> [res add in place | new dense channels appended]
+        emit_conv(B, c3, Act{Bb, r, n, Ho, Wo, r}, nullptr, 0, 1, 1, 1, 1, 0, 0, Ho, Wo, S, ctot,
+                  EPI_RES, S, ctot, S ? S + (size_t)(bw + dense) * es : nullptr, ctot, bw,
+                  (const float*)b3.mean->p, (const float*)b3.inv->p);
+      }
       dense += inc;
       B.tap(S, n, Ho, Wo, bw + dense, ctot);
     }
@@ -1546,6 +1614,7 @@ static hipError_t run_op(vox_model* m, const Op& op, hipStream_t s) {
     case 24: return launch_chain_fused(op.ch, s);
     case 25: return launch_conv3_rw(op.cp, m->num_cu, s);
     case 30: return launch_conv3_ks(op.cp, m->num_cu, s);
+    case 31: return launch_dpn_block(op.dq, s);
     case 26: return launch_conv3_utt(op.cp, m->num_cu, s);
     case 27: return launch_conv1x1_smallk(op.cp, s);
     case 29: return launch_conv1x1_nw(op.cp, m->num_cu, s);
@@ -1815,6 +1884,8 @@ extern "C" int vox_profile(vox_model* m, const float* d_x, int n, int t, int f, 
         tag |= (1 << 29) | (1 << 18) | (1 << 19);
       else if (o.type == 30)
         tag |= (1 << 29) | (1 << 18) | (1 << 16);
+      else if (o.type == 31)
+        tag |= (1 << 28) | (1 << 19);
       else if (o.type == 8)
         tag |= (o.cl.wco << 4) | (o.cl.wpx << 8) | (((o.cp.cinp + 31) / 32) << 16) | (1 << 20);
       else if (o.type == 0 || o.type == 5)
@@ -1846,7 +1917,7 @@ extern "C" int vox_plan_describe(vox_model* m, const float* d_x, int n, int t, i
                              "win", "rr", "gemm", "chain", "stem", "bneck", "chainrows", "splits2",
                              "cvt16", "atttanh", "attpool", "gemmpipe", "gconv", "conv3pipe",
                              "gemmwide", "s2fused", "-", "chainfused", "conv3rw", "conv3utt",
-                             "smallk", "conv3s2r", "nw", "conv3ks"};
+                             "smallk", "conv3s2r", "nw", "conv3ks", "dpnblock"};
   for (const Op& o : m->plan) {
     char line[256];
     const ConvParams& p = o.cp;
@@ -1863,6 +1934,10 @@ extern "C" int vox_plan_describe(vox_model* m, const float* d_x, int n, int t, i
       std::snprintf(line, sizeof(line), "bneck N=%d H=%d W=%d Cin=%d C=%d w=%d split=%d seg=%d nseg=%d flops=%.4g bytes=%.4g\n",
                     o.bq.N, o.bq.H, o.bq.W, o.cin, o.C, o.cl.wco, o.S, o.bq.seg, o.bq.nseg, o.flops,
                     o.bytes);
+    else if (o.type == 31)
+      std::snprintf(line, sizeof(line), "dpnblock N=%d H=%d W=%d Cin=%d Cout=%d bw=%d from_a=%d seg=%d nseg=%d flops=%.4g bytes=%.4g\n",
+                    o.dq.N, o.dq.H, o.dq.W, o.dq.cin, o.dq.cout, o.dq.bw, o.dq.from_a, o.dq.seg, o.dq.nseg,
+                    o.flops, o.bytes);
     else if (o.type == 19)
       std::snprintf(line, sizeof(line), "gconv N=%d H=%d W=%d C=%d gw=%d Ho=%d Wo=%d st=%d rs=%d seg=%d nseg=%d flops=%.4g bytes=%.4g\n",
                     o.gq.N, o.gq.H, o.gq.W, o.gq.C, o.gq.gw, o.gq.Ho, o.gq.Wo, o.gq.sh,

@@ -208,6 +208,29 @@ int gconv_rs(const GconvParams& p);
 int gconv_lds(const GconvParams& p);
 hipError_t launch_gconv(const GconvParams& p, hipStream_t s);
 
+// Fused DPN stage-1 dual-path block (dpnblk.hip): 1x1a (cin -> 128, BN+ReLU
+// prologue m1/i1) -> grouped 3x3 (gconv3x3_rows' expanded weights, gw <= 16,
+// prologue m2/i2) -> 1x1c (128 -> cout <= 96, prologue m3/i3); channels < bw
+// get the residual x[.., c] and go to y (in place over x allowed), the rest to
+// y2[c - bw].  Stride 1, 65 <= W <= 80.  Two launches: the segment-halo rows'
+// 1x1a into `halo` (dpn_block_halo_bytes), then the row-streamed block.
+// from_a: x is the block's 1x1a output (cin = 128, w1/m1/i1 unused, one launch,
+// no halo): the grouped 3x3 + 1x1c only.  The residual is res[.., c < bw].
+struct DpnBlockParams {
+  const void* x; int ldx; int cin;
+  const void* res; int ldr;
+  int from_a;
+  const void* w1; int kp1; const float* m1; const float* i1;   // paired-row [>=128][kp1]
+  const void* wg; const float* m2; const float* i2;            // [8][5][64][8]
+  const void* w3; int kp3; const float* m3; const float* i3;   // paired-row [>=96][kp3 = 128]
+  void* y; void* y2; int ldy; int bw, cout;
+  void* halo;
+  int N, H, W, seg, nseg;
+};
+int dpn_block_ok(const DpnBlockParams& p);
+size_t dpn_block_halo_bytes(const DpnBlockParams& p);
+hipError_t launch_dpn_block(const DpnBlockParams& p, hipStream_t s);
+
 // DPN68's 10-channel 1x1 convs with the BN+ReLU prologue (kernels.hip)
 int conv1x1_smallk_ok(const ConvParams& p);
 hipError_t launch_conv1x1_smallk(const ConvParams& p, hipStream_t s);
