@@ -193,6 +193,8 @@ struct Op {
   BneckParams bq{};  // type 12: Cin (cin), C, w (cl.wco), split (S)
   GconvParams gq{};  // type 19
   DpnBlockParams dq{};  // type 31
+  const float* in_mean = nullptr;  // type 2: input BN+ReLU fused into the pool (DPN68)
+  const float* in_inv = nullptr;
   int cin = 0;
   double flops = 0, bytes = 0;
 };
@@ -260,6 +262,8 @@ struct vox_model {
   int no_nw = 0;           // VOXEMB_NO_NW: narrow 1x1s on conv1x1_rr instead of conv1x1_nw
   int no_dpn_block = 0;    // VOXEMB_NO_DPN_BLOCK: DPN stage-1 blocks as 1x1a / gconv / 1x1c launches
   int dpn_nseg = 0;        // VOXEMB_DPN_NSEG: force dpn_block_rows' segments per utterance (tests)
+  int dpn_dbg = 0;         // VOXEMB_DPN_DBG: dpn_block_rows diagnostics (VOX_DIAG builds)
+  int no_pool_pro = 0;     // VOXEMB_NO_POOL_PRO: DPN68's final BN+ReLU as its own pass before the pool
   int pro_min_cout = 192;  // VOXEMB_PRO_MIN_COUT: narrowest prologue 1x1 on gemm1x1_ws
   int gemm_var = 0;        // VOXEMB_GEMM_VAR: -1 = gemm1x1_wide instead of gemm1x1_ws
                            // (bitwise A/B); other values are diagnostics (VOX_DIAG builds)
@@ -301,6 +305,8 @@ static const PlanEnv kPlanEnv[] = {
     {"VOXEMB_NO_NW", &vox_model::no_nw},
     {"VOXEMB_NO_DPN_BLOCK", &vox_model::no_dpn_block},
     {"VOXEMB_DPN_NSEG", &vox_model::dpn_nseg},
+    {"VOXEMB_DPN_DBG", &vox_model::dpn_dbg},
+    {"VOXEMB_NO_POOL_PRO", &vox_model::no_pool_pro},
     {"VOXEMB_PRO_MIN_COUT", &vox_model::pro_min_cout},
     {"VOXEMB_GEMM_VAR", &vox_model::gemm_var},
     {"VOXEMB_GEMM_MIN_K", &vox_model::gemm_min_k},
@@ -829,13 +835,17 @@ static void emit_conv(Builder& B, const ConvW& cw, Act x, const void* x2, int ld
   B.ops->push_back(op);
 }
 
-static void emit_pool(Builder& B, Act x, float* out, const BNW& bn) {
+static void emit_pool(Builder& B, Act x, float* out, const BNW& bn, const BNW* in_bn = nullptr) {
   Op op;
   op.kind = OP_POOL;
   op.type = 2;
   op.src = x.p; op.N = x.N; op.H = x.H; op.W = x.W; op.C = x.C;
   op.mean = (const float*)bn.mean->p;
   op.inv = (const float*)bn.inv->p;
+  if (in_bn) {
+    op.in_mean = (const float*)in_bn->mean->p;
+    op.in_inv = (const float*)in_bn->inv->p;
+  }
   op.out = out;
   op.bytes = (double)es_of(B.m) * x.N * x.H * x.W * x.C + 4.0 * x.N * x.W * 2 * x.C;
   B.ops->push_back(op);
@@ -1453,6 +1463,7 @@ static int build_dpn(Builder& B, const float* x, int n, int t, float* out) {
         dq.y = S; dq.y2 = S ? S + (size_t)(bw + dense) * es : nullptr; dq.ldy = ctot;
         dq.bw = bw; dq.cout = c3.cout;
         dq.N = n; dq.H = Ho; dq.W = Wo;
+        dq.dbg = m->dpn_dbg;
         // one workgroup per CU (118 KB LDS): enough segments to cover the chip,
         // each >= 8 rows (the first and last rows' 3x3 windows reach into the
         // neighbours: their h1 rows are computed twice)
@@ -1534,9 +1545,16 @@ static int build_dpn(Builder& B, const float* x, int n, int t, float* out) {
     H = Ho;
     W = Wo;
   }
-  // concat_bn_relu: a BN+ReLU pass, fused as a 1x1 identity is wasteful;
-  // apply it inside the pool via a dedicated BN-ReLU elementwise op.
+  // concat_bn_relu (dpn_model.py:24-29): applied by the pool to every element
+  // it reads (the bits of the in-place BN+ReLU pass, without its 2 x 160 MB
+  // round trip at B = 64); a separate pass only if the map is not packed
   const BNW& fb = m->bns[bi++];
+  float* pooled = (float*)B.base(S_POOL, (size_t)n * W * 2 * cur.C * 4);
+  if (cur.ld == cur.C && !m->no_pool_pro) {
+    emit_pool(B, cur, pooled, m->head_bn1, &fb);
+    emit_head(B, pooled, n, out);
+    return VOX_OK;
+  }
   {
     Op op;
     op.kind = OP_OTHER;
@@ -1546,7 +1564,6 @@ static int build_dpn(Builder& B, const float* x, int n, int t, float* out) {
     op.bytes = 2.0 * es * n * H * W * cur.C;
     B.ops->push_back(op);
   }
-  float* pooled = (float*)B.base(S_POOL, (size_t)n * W * 2 * cur.C * 4);
   emit_pool(B, cur, pooled, m->head_bn1);
   emit_head(B, pooled, n, out);
   return VOX_OK;
@@ -1631,7 +1648,9 @@ static hipError_t run_op(vox_model* m, const Op& op, hipStream_t s) {
     case 1:
       return launch_splitk_reduce(op.part, op.S, op.M, op.coutp, op.cout, op.mean, op.inv,
                                   op.flags, op.out, op.ldo, s);
-    case 2: return launch_stats_pool(m->dt, op.src, op.N, op.H, op.W, op.C, op.mean, op.inv, op.out, s);
+    case 2:
+      return launch_stats_pool(m->dt, op.src, op.N, op.H, op.W, op.C, op.mean, op.inv, op.out, s,
+                               op.in_mean, op.in_inv);
     case 3:
       return launch_avgpool3s2(m->dt, op.src, op.lds, op.N, op.H, op.W, op.C, op.dst, op.ldd, op.Ho,
                                op.Wo, s);
@@ -1690,9 +1709,9 @@ extern "C" int vox_load_blob(const void* blob, size_t nbytes, int device, int pr
 #ifndef VOX_DIAG
   // diagnostic variants skip work (wrong results) and are compiled only into
   // the VOX_DIAG build (libvoxemb_diag.so, build_native.py --diag)
-  if (m->bneck_dbg || (m->gemm_var != 0 && m->gemm_var != 1 && m->gemm_var != -1) ||
+  if (m->bneck_dbg || m->dpn_dbg || (m->gemm_var != 0 && m->gemm_var != 1 && m->gemm_var != -1) ||
       std::getenv("VOXEMB_CONV3_RW_DBG"))
-    return fail(VOX_EINVAL, "diagnostic switches (VOXEMB_BNECK_DBG / VOXEMB_GEMM_VAR / "
+    return fail(VOX_EINVAL, "diagnostic switches (VOXEMB_BNECK_DBG / VOXEMB_DPN_DBG / VOXEMB_GEMM_VAR / "
                             "VOXEMB_CONV3_RW_DBG) need the VOX_DIAG build (libvoxemb_diag.so)");
 #endif
   if ((rc = load_weights(m.get(), ts))) return rc;
@@ -1897,6 +1916,13 @@ extern "C" int vox_profile(vox_model* m, const float* d_x, int n, int t, int f, 
   return nops;
 }
 
+// diagnostics: dpn_block_rows clock stamps (8 waves x 256 steps x 8 u64), see dpnblk.hip
+extern "C" int vox_debug_dpn_trace(void* dst, size_t bytes) {
+  if (!dst) return fail(VOX_EINVAL, "null argument");
+  HIPCHK(dpn_trace_read(dst, bytes));
+  return VOX_OK;
+}
+
 // diagnostics: bneck_fused clock stamps (8 waves x 512 steps x 4 u64), see bneck.hip
 extern "C" int vox_debug_bneck_trace(void* dst, size_t bytes) {
   if (!dst) return fail(VOX_EINVAL, "null argument");
@@ -1958,6 +1984,9 @@ extern "C" int vox_plan_describe(vox_model* m, const float* d_x, int n, int t, i
       std::snprintf(line, sizeof(line), "chain wco=%d wpx=%d N=%d H=%d W=%d w=%d nst=%d R=%d lds=%d flops=%.4g bytes=%.4g\n",
                     o.cl.wco, o.cl.wpx, o.ch.N, o.ch.H, o.ch.W, o.ch.w, o.ch.nst, o.ch.R, o.ch.lds,
                     o.flops, o.bytes);
+    else if (o.type == 2)
+      std::snprintf(line, sizeof(line), "pool N=%d H=%d W=%d C=%d pro=%d bytes=%.4g\n", o.N, o.H,
+                    o.W, o.C, o.in_mean ? 1 : 0, o.bytes);
     else
       std::snprintf(line, sizeof(line), "%s N=%d H=%d W=%d C=%d bytes=%.4g\n", tn[o.type], o.N,
                     o.H, o.W, o.C, o.bytes);

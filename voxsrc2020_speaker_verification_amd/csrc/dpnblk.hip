@@ -49,6 +49,10 @@
 namespace vox {
 
 __device__ uint4 g_db_zero[2] = {};   // source of masked loads (channels >= cin, pixels >= W)
+__device__ uint4 g_db_sink[64];       // destination of masked lanes' stores
+// diagnostics (VOXEMB_DPN_DBG & 256, VOX_DIAG builds): per-step shader-clock
+// stamps of workgroup 0's waves [8 waves][256 steps][8 stamps]
+__device__ unsigned long long g_db_trace[8 * 256 * 8];
 
 namespace {
 constexpr int DB_THREADS = 512;
@@ -56,9 +60,10 @@ constexpr int DB_R = 128;   // 1x1a / grouped 3x3 width
 constexpr int DB_PXS = 18;  // X1 / H2 units per pixel (16 + 2: 18 = 2 mod 16, conflict-free b128 reads)
 constexpr int DB_KS = 4;    // k-steps of 32: 1x1a (cin <= 128) and 1x1c (K = 128)
 constexpr int DB_TPR = 5;   // 16-pixel tiles per row (65 <= W <= 80)
+constexpr int DB_RXS = 10;  // RES units per pixel (8 + 2: 10 = 10 mod 16, conflict-free b128 reads)
 
 struct DbGeo {
-  int spw, rowb, zero, x1, h2, tb, lds;
+  int spw, rowb, zero, x1, h2, res, tb, lds;
 };
 __host__ __device__ inline DbGeo db_geo(int W) {
   DbGeo g{};
@@ -69,7 +74,8 @@ __host__ __device__ inline DbGeo db_geo(int W) {
   g.zero = 3 * g.rowb;                 // zero line of the paired tap 9 (512 B per tile)
   g.x1 = g.zero + 512 * DB_TPR + 1024; // + slack: masked tail columns read past the ring
   g.h2 = g.x1 + 16 * DB_TPR * DB_PXS * 16;
-  g.tb = g.h2 + 16 * DB_TPR * DB_PXS * 16;   // BN tables: m1 i1 -m2 i2 m3 i3 (128 floats each)
+  g.res = g.h2 + 16 * DB_TPR * DB_PXS * 16;  // residual rows (bw <= 64 channels), 3 slots
+  g.tb = g.res + 3 * 16 * DB_TPR * DB_RXS * 16;   // BN tables: m1 i1 -m2 i2 m3 i3 (128 floats each)
   g.lds = g.tb + 6 * DB_R * 4;
   return g;
 }
@@ -130,13 +136,18 @@ __global__ __launch_bounds__(DB_THREADS) void dpn_block_rows(DpnBlockParams p) {
   }
   __syncthreads();
   const uint4* zl = g_db_zero;
+  const bool trace = (VOX_DBG(p) & 256) && blockIdx.x == 0 && lane == 0;
+  auto stamp = [&](int o, int i) __attribute__((always_inline)) {
+    if (trace && o - s0 < 256) g_db_trace[(wave * 256 + (o - s0)) * 8 + i] = __builtin_amdgcn_s_memtime();
+  };
   auto load_row = [&](int r, uint4 (&v)[U]) __attribute__((always_inline)) {
     const bf16_t* __restrict__ Xr = Xn + (size_t)r * rowe;   // wave-uniform base
 #pragma unroll
     for (int i = 0; i < U; ++i)
       v[i] = *((upx[i] >= 0 && cval) ? reinterpret_cast<const uint4*>(Xr + uoff[i]) : zl);
   };
-  auto stage_x1 = [&](const uint4 (&v)[U]) __attribute__((always_inline)) {
+  // (mode 0) the row's raw first bw channels also go to RES[par] for its 1x1c residual
+  auto stage_x1 = [&](const uint4 (&v)[U], int par) __attribute__((always_inline)) {
     float pm[8], pi[8];
     *reinterpret_cast<f32x4*>(pm) = *reinterpret_cast<const f32x4*>(tb + 8 * ch8);
     *reinterpret_cast<f32x4*>(pm + 4) = *reinterpret_cast<const f32x4*>(tb + 8 * ch8 + 4);
@@ -150,6 +161,8 @@ __global__ __launch_bounds__(DB_THREADS) void dpn_block_rows(DpnBlockParams p) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) o[e] = (bf16_t)fmaxf(((float)b[e] - pm[e]) * pi[e], 0.f);
       *reinterpret_cast<bf16x8*>(smem + geo.x1 + (upx[i] * DB_PXS + ch8) * 16) = o;
+      if (8 * ch8 < p.bw)
+        *reinterpret_cast<uint4*>(smem + geo.res + ((par * 16 * TPR + upx[i]) * DB_RXS + ch8) * 16) = v[i];
     }
   };
 
@@ -265,7 +278,7 @@ __global__ __launch_bounds__(DB_THREADS) void dpn_block_rows(DpnBlockParams p) {
       if (r < 0 || r >= H) continue;
       uint4 v[U];
       load_row(r, v);
-      stage_x1(v);
+      stage_x1(v, 0);
       __syncthreads();
       gemm1a(0);
       __syncthreads();
@@ -348,15 +361,25 @@ __global__ __launch_bounds__(DB_THREADS) void dpn_block_rows(DpnBlockParams p) {
     const int ch3 = 32 * q3 + 8 * g;
     bf16_t* __restrict__ Yn = reinterpret_cast<bf16_t*>(p.y) + (size_t)n * H * W * p.ldy;
     bf16_t* __restrict__ Y2n = reinterpret_cast<bf16_t*>(p.y2) + (size_t)n * H * W * p.ldy;
+    // mode 2: the residual rows (p.res, first bw channels) are prefetched with
+    // the ring rows: unit u = tid + 512 i -> (pixel u / 8, chunk u % 8)
+    constexpr int UR = (128 * TPR + DB_THREADS - 1) / DB_THREADS;
     const bf16_t* __restrict__ Rn = reinterpret_cast<const bf16_t*>(p.res) + (size_t)n * H * W * p.ldr;
-    uint4 rv[3];
-    auto load_res = [&](int o) __attribute__((always_inline)) {
-      const bf16_t* __restrict__ Rr = Rn + (size_t)o * W * p.ldr;
+    auto load_res = [&](int r, uint4 (&v)[UR]) __attribute__((always_inline)) {
+      const bf16_t* __restrict__ Rr = Rn + (size_t)r * W * p.ldr;
 #pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        const int px = 16 * (t3 + j) + col;
-        const bool ok = j < nt3 && px < W && ch3 < p.bw;
-        rv[j] = *(ok ? reinterpret_cast<const uint4*>(Rr + (size_t)px * p.ldr + ch3) : zl);
+      for (int i = 0; i < UR; ++i) {
+        const int u = tid + DB_THREADS * i, px = u >> 3, c8 = u & 7;
+        const bool ok = px < W && 8 * c8 < p.bw;
+        v[i] = *(ok ? reinterpret_cast<const uint4*>(Rr + (size_t)px * p.ldr + 8 * c8) : zl);
+      }
+    };
+    auto stage_res = [&](const uint4 (&v)[UR], int par) __attribute__((always_inline)) {
+#pragma unroll
+      for (int i = 0; i < UR; ++i) {
+        const int u = tid + DB_THREADS * i, px = u >> 3, c8 = u & 7;
+        if (px < W && 8 * c8 < p.bw)
+          *reinterpret_cast<uint4*>(smem + geo.res + ((par * 16 * TPR + px) * DB_RXS + c8) * 16) = v[i];
       }
     };
     auto gemm1c_t = [&](auto NT_, int o) __attribute__((always_inline)) {
@@ -373,22 +396,27 @@ __global__ __launch_bounds__(DB_THREADS) void dpn_block_rows(DpnBlockParams p) {
           acc[0][j] = mfma_step(a3[0][s], b, acc[0][j]);
           acc[1][j] = mfma_step(a3[1][s], b, acc[1][j]);
         }
-      if (ch3 >= p.cout) return;
+      const int par = (o - s0) % 3;
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
         const int px = 16 * (t3 + j) + col;
-        if (px >= W) continue;
-        const bf16x8 r = __builtin_bit_cast(bf16x8, rv[j]);
+        // residual below bw (RES row o), +0.0 on the dense channels (conv1x1_nw)
+        const bf16x8 r = ch3 < p.bw ? *reinterpret_cast<const bf16x8*>(
+                                          smem + geo.res + ((par * 16 * TPR + px) * DB_RXS + (ch3 >> 3)) * 16)
+                                    : bf16x8{};
         bf16x8 o8;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           float v = e < 4 ? acc[0][j][e] : acc[1][j][e - 4];
-          v += (float)r[e];   // residual below bw, +0.0 on the dense channels (conv1x1_nw)
+          v += (float)r[e];
           o8[e] = (bf16_t)v;
         }
+        // every lane stores (masked ones into the sink): no divergent store
+        // branches, so the compiler's vmcnt counts stay exact
         const size_t pix = (size_t)o * W + px;
         bf16_t* dst = ch3 < p.bw ? Yn + pix * p.ldy + ch3 : Y2n + pix * p.ldy + (ch3 - p.bw);
-        *reinterpret_cast<bf16x8*>(dst) = o8;
+        void* d = (ch3 < p.cout && px < W) ? (void*)dst : (void*)&g_db_sink[lane];
+        *reinterpret_cast<bf16x8*>(d) = o8;
       }
     };
     using N1 = std::integral_constant<int, 1>;
@@ -404,9 +432,11 @@ __global__ __launch_bounds__(DB_THREADS) void dpn_block_rows(DpnBlockParams p) {
     using P1 = std::integral_constant<int, 1>;
     if constexpr (FROM_A) {
       // ring rows straight from the (immutable) 1x1a map: rows s0 - 1 .. s1,
-      // zeros outside the image; prefetched two rows ahead
+      // zeros outside the image.  Ring row o + 2 and RES row o + 2 are staged
+      // in step o between the 3x3 and the 1x1c (their register prefetch, two
+      // rows ahead, has long landed; the wait then covers no fresh stores).
       const int last = min(s1, H - 1);
-      uint4 pf[2][U];
+      uint4 pf[2][U], rp[2][UR];
       if (s0 > 0) {
         load_row(s0 - 1, pf[1]);
         stage_ring(pf[1], ring_off(s0 - 1));
@@ -414,22 +444,37 @@ __global__ __launch_bounds__(DB_THREADS) void dpn_block_rows(DpnBlockParams p) {
         fill_row(ring_off(s0 - 1), -1);
       }
       load_row(s0, pf[0]);
+      load_res(s0, rp[0]);
       if (s0 + 1 <= last) load_row(s0 + 1, pf[1]);
+      if (s0 + 1 < s1) load_res(s0 + 1, rp[1]);
       stage_ring(pf[0], ring_off(s0));
+      stage_res(rp[0], 0);
       if (s0 + 2 <= last) load_row(s0 + 2, pf[0]);
+      if (s0 + 2 < s1) load_res(s0 + 2, rp[0]);
+      if (s0 + 1 < H) stage_ring(pf[1], ring_off(s0 + 1));
+      else fill_row(ring_off(s0 + 1), -1);
+      if (s0 + 1 < s1) stage_res(rp[1], 1);
+      if (s0 + 3 <= last) load_row(s0 + 3, pf[1]);
+      if (s0 + 3 < s1) load_res(s0 + 3, rp[1]);
+      __syncthreads();
       auto step = [&](auto PS, int o) __attribute__((always_inline)) {
         constexpr int PI = decltype(PS)::value;
-        load_res(o);
-        if (o + 1 < H) {
-          stage_ring(pf[PI ^ 1], ring_off(o + 1));
-          if (o + 3 <= last) load_row(o + 3, pf[PI ^ 1]);
-        } else {
-          fill_row(ring_off(o + 1), -1);
+        gconv_row(o);      // ring rows o - 1 .. o + 1
+        __syncthreads();   // H2 complete; ring slot of row o - 1 free
+        if (o + 2 <= s1) {
+          if (o + 2 < H) {
+            stage_ring(pf[PI], ring_off(o + 2));
+            if (o + 4 <= last) load_row(o + 4, pf[PI]);
+          } else {
+            fill_row(ring_off(o + 2), -1);
+          }
         }
-        __syncthreads();   // ring rows o - 1 .. o + 1 complete
-        gconv_row(o);
-        __syncthreads();   // H2 complete
-        gemm1c(o);
+        if (o + 2 < s1) {
+          stage_res(rp[PI], (o + 2 - s0) % 3);
+          if (o + 4 < s1) load_res(o + 4, rp[PI]);
+        }
+        gemm1c(o);         // RES row o
+        __syncthreads();   // ring row o + 2, RES row o + 2 staged; H2 free
       };
       for (int o = s0; o < s1; o += 2) {
         step(P0{}, o);
@@ -437,33 +482,47 @@ __global__ __launch_bounds__(DB_THREADS) void dpn_block_rows(DpnBlockParams p) {
       }
       return;
     }
-    // ---- prologue: ring rows s0 - 1 (halo / zeros) and s0 (computed)
+    // ---- prologue: ring rows s0 - 1 (halo / zeros) and s0 (computed), X1 = row s0 + 1
     fill_row(ring_off(s0 - 1), s0 > 0 ? 0 : -1);
     uint4 pf[2][U];
     load_row(s0, pf[0]);
     if (s0 + 1 < s1) load_row(s0 + 1, pf[1]);
-    stage_x1(pf[0]);
+    stage_x1(pf[0], 0);
     if (s0 + 2 < s1) load_row(s0 + 2, pf[0]);
     __syncthreads();
     gemm1a(ring_off(s0));
+    __syncthreads();
+    if (s0 + 1 < s1) {
+      stage_x1(pf[1], 1);
+      if (s0 + 3 < s1) load_row(s0 + 3, pf[1]);
+    }
+    __syncthreads();
 
-    // step o: h1 of row o + 1 into the ring, 3x3 of row o into H2, 1x1c of row
-    // o to HBM.  Row o + 1's input is in pf[PI ^ 1] (PI = (o - s0) & 1).
+    // step o: h1 of row o + 1 (X1) into the ring, 3x3 of row o into H2, then
+    // row o + 2 into X1 / RES (its register prefetch, two rows ahead, has long
+    // landed, and the wait for it covers no fresh stores) and the 1x1c of row
+    // o to HBM.  Row o + 2's input is in pf[PI] (PI = (o - s0) & 1).
     auto step = [&](auto PS, int o) __attribute__((always_inline)) {
       constexpr int PI = decltype(PS)::value;
-      load_res(o);
-      if (o + 1 < s1) {
-        stage_x1(pf[PI ^ 1]);
-        if (o + 3 < s1) load_row(o + 3, pf[PI ^ 1]);
-      } else {
-        fill_row(ring_off(o + 1), o + 1 < H ? 1 : -1);
-      }
-      __syncthreads();   // X1 staged; ring slot of row o + 1 free (read last in step o - 1)
+      stamp(o, 0);
       if (o + 1 < s1) gemm1a(ring_off(o + 1));
-      __syncthreads();   // ring rows o - 1 .. o + 1 complete
+      else fill_row(ring_off(o + 1), o + 1 < H ? 1 : -1);
+      stamp(o, 1);
+      __syncthreads();   // ring rows o - 1 .. o + 1 complete; X1 free
+      stamp(o, 2);
       gconv_row(o);
+      stamp(o, 3);
       __syncthreads();   // H2 complete
+      stamp(o, 4);
+      if (o + 2 < s1) {
+        stage_x1(pf[PI], (o + 2 - s0) % 3);
+        if (o + 4 < s1) load_row(o + 4, pf[PI]);
+      }
+      stamp(o, 5);
       gemm1c(o);
+      stamp(o, 6);
+      __syncthreads();   // X1 = row o + 2; H2 free
+      stamp(o, 7);
     };
     for (int o = s0; o < s1; o += 2) {
       step(P0{}, o);
@@ -483,6 +542,11 @@ int dpn_block_ok(const DpnBlockParams& p) {
 
 size_t dpn_block_halo_bytes(const DpnBlockParams& p) {
   return (size_t)p.N * p.nseg * 2 * db_geo(p.W).rowb;
+}
+
+hipError_t dpn_trace_read(void* dst, size_t bytes) {
+  if (bytes > sizeof(g_db_trace)) bytes = sizeof(g_db_trace);
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_db_trace), bytes, 0, hipMemcpyDeviceToHost);
 }
 
 hipError_t launch_dpn_block(const DpnBlockParams& p, hipStream_t s) {

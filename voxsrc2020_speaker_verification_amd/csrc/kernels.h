@@ -226,7 +226,9 @@ struct DpnBlockParams {
   void* y; void* y2; int ldy; int bw, cout;
   void* halo;
   int N, H, W, seg, nseg;
+  int dbg;   // diagnostics (VOXEMB_DPN_DBG, VOX_DIAG builds): 256 = clock stamps
 };
+hipError_t dpn_trace_read(void* dst, size_t bytes);
 int dpn_block_ok(const DpnBlockParams& p);
 size_t dpn_block_halo_bytes(const DpnBlockParams& p);
 hipError_t launch_dpn_block(const DpnBlockParams& p, hipStream_t s);
@@ -239,8 +241,10 @@ hipError_t launch_splitk_reduce(const float* partial, int S, int M, int coutp, i
                                 const float* mean, const float* inv, int flags,
                                 float* out, int ldo, hipStream_t s);
 
+// in_mean / in_inv: optional input BN+ReLU (DPN68's concat_bn_relu) fused into the read
 hipError_t launch_stats_pool(DType t, const void* x, int N, int H, int W, int C,
-                             const float* mean, const float* inv, float* out, hipStream_t s);
+                             const float* mean, const float* inv, float* out, hipStream_t s,
+                             const float* in_mean = nullptr, const float* in_inv = nullptr);
 
 hipError_t launch_avgpool3s2(DType t, const void* x, int ldx, int N, int H, int W, int C,
                              void* y, int ldy, int Ho, int Wo, hipStream_t s);

@@ -1346,12 +1346,18 @@ hipError_t launch_splitk_reduce(const float* partial, int S, int M, int coutp, i
 // slice partials are combined in fixed order through LDS (deterministic),
 // first for the mean and then for the centred second moment (two-pass, as
 // tf.nn.moments).  out[n][w*2C + c] = mean, out[n][w*2C + C + c] = std.
+// in_mean / in_inv (optional): an input BN+ReLU applied to every element as it
+// is read, rounded to T: the bits of DPN68's in-place concat_bn_relu pass
+// (bnrelu_k, dpn_model.py:24-29) followed by the pool, without the extra
+// read + write of the map.
 template <typename T, int VN, int TS>
 __global__ __launch_bounds__(64 * TS) void stats_pool_k(const T* __restrict__ x, int N, int H,
                                                         int W, int C,
                                                         const float* __restrict__ mean,
                                                         const float* __restrict__ inv,
-                                                        float* __restrict__ out) {
+                                                        float* __restrict__ out,
+                                                        const float* __restrict__ in_mean,
+                                                        const float* __restrict__ in_inv) {
   __shared__ float red[TS][64][VN];
   __shared__ float mu_s[64][VN];
   const int cx = threadIdx.x & 63, ts = threadIdx.x >> 6;
@@ -1367,6 +1373,17 @@ __global__ __launch_bounds__(64 * TS) void stats_pool_k(const T* __restrict__ x,
   }
   const size_t rowstride = (size_t)W * C;
   const T* base = x + ((size_t)n * H * W + w) * C + (size_t)ch * VN;
+  const bool pro = in_mean != nullptr;
+  float pm[VN], pi[VN];
+#pragma unroll
+  for (int e = 0; e < VN; ++e) {
+    pm[e] = pro ? in_mean[ch * VN + e] : 0.f;
+    pi[e] = pro ? in_inv[ch * VN + e] : 1.f;
+  }
+  // element e of a row as the pool sees it (bnrelu_k's rounding when pro)
+  auto elt = [&](float raw, int e) __attribute__((always_inline)) {
+    return pro ? (float)(T)fmaxf((raw - pm[e]) * pi[e], 0.f) : raw;
+  };
   // the first RM rows of this slice stay in registers for the second pass (the
   // re-read was the kernel's second HBM/L2 stream); same summation order
   constexpr int RM = 8;
@@ -1383,10 +1400,10 @@ __global__ __launch_bounds__(64 * TS) void stats_pool_k(const T* __restrict__ x,
         if constexpr (sizeof(T) == 2 && VN == 8) {
           const bf16x8 r = ld16(q);
 #pragma unroll
-          for (int e = 0; e < VN; ++e) v[i][e] = (float)r[e];
+          for (int e = 0; e < VN; ++e) v[i][e] = elt((float)r[e], e);
         } else {
 #pragma unroll
-          for (int e = 0; e < VN; ++e) v[i][e] = (float)q[e];
+          for (int e = 0; e < VN; ++e) v[i][e] = elt((float)q[e], e);
         }
 #pragma unroll
         for (int e = 0; e < VN; ++e) s[e] += v[i][e];
@@ -1397,7 +1414,7 @@ __global__ __launch_bounds__(64 * TS) void stats_pool_k(const T* __restrict__ x,
     for (int h = ts + RM * TS; h < H; h += TS) {
       const T* q = base + (size_t)h * rowstride;
 #pragma unroll
-      for (int e = 0; e < VN; ++e) s[e] += (float)q[e];
+      for (int e = 0; e < VN; ++e) s[e] += elt((float)q[e], e);
     }
   }
 #pragma unroll
@@ -1431,7 +1448,7 @@ __global__ __launch_bounds__(64 * TS) void stats_pool_k(const T* __restrict__ x,
       const T* q = base + (size_t)h * rowstride;
 #pragma unroll
       for (int e = 0; e < VN; ++e) {
-        float d = (float)q[e] - mu[e];
+        float d = elt((float)q[e], e) - mu[e];
         s[e] += d * d;
       }
     }
@@ -1613,10 +1630,11 @@ __global__ __launch_bounds__(256) void stats_pool_h2(const bf16_t* __restrict__ 
 
 template <typename T, int VN>
 static hipError_t stats_pool_ts(const T* x, int N, int H, int W, int C, const float* mean,
-                                const float* inv, float* out, hipStream_t s) {
+                                const float* inv, float* out, const float* in_mean,
+                                const float* in_inv, hipStream_t s) {
   const int64_t cols = (int64_t)N * W * (C / VN);
   if constexpr (sizeof(T) == 2 && VN == 8) {
-    if (H <= 32) {
+    if (H <= 32 && !in_mean) {
 #ifdef VOX_DIAG
       static const int vn8 = [] { const char* e = std::getenv("VOXEMB_POOL_VN8"); return e ? std::atoi(e) : 0; }();
       if (vn8 && H <= 25 && H > 16) {   // A/B: 8 channels (16-B loads) per thread
@@ -1650,29 +1668,30 @@ static hipError_t stats_pool_ts(const T* x, int N, int H, int W, int C, const fl
   // batch size past ~680 utterances)
   if (H >= 64) {
     hipLaunchKernelGGL((stats_pool_k<T, VN, 8>), dim3(blocks), dim3(64 * 8), 0, s, x, N, H, W, C,
-                       mean, inv, out);
+                       mean, inv, out, in_mean, in_inv);
   } else if (H >= 16) {
     hipLaunchKernelGGL((stats_pool_k<T, VN, 4>), dim3(blocks), dim3(64 * 4), 0, s, x, N, H, W, C,
-                       mean, inv, out);
+                       mean, inv, out, in_mean, in_inv);
   } else {
     hipLaunchKernelGGL((stats_pool_k<T, VN, 1>), dim3(blocks), dim3(64), 0, s, x, N, H, W, C,
-                       mean, inv, out);
+                       mean, inv, out, in_mean, in_inv);
   }
   return hipGetLastError();
 }
 
 hipError_t launch_stats_pool(DType t, const void* x, int N, int H, int W, int C,
-                             const float* mean, const float* inv, float* out, hipStream_t s) {
+                             const float* mean, const float* inv, float* out, hipStream_t s,
+                             const float* in_mean, const float* in_inv) {
   if (t == BF16) {
     if (C % 8 == 0)
-      return stats_pool_ts<bf16_t, 8>((const bf16_t*)x, N, H, W, C, mean, inv, out, s);
+      return stats_pool_ts<bf16_t, 8>((const bf16_t*)x, N, H, W, C, mean, inv, out, in_mean, in_inv, s);
     if (C % 2 == 0)
-      return stats_pool_ts<bf16_t, 2>((const bf16_t*)x, N, H, W, C, mean, inv, out, s);
-    return stats_pool_ts<bf16_t, 1>((const bf16_t*)x, N, H, W, C, mean, inv, out, s);
+      return stats_pool_ts<bf16_t, 2>((const bf16_t*)x, N, H, W, C, mean, inv, out, in_mean, in_inv, s);
+    return stats_pool_ts<bf16_t, 1>((const bf16_t*)x, N, H, W, C, mean, inv, out, in_mean, in_inv, s);
   }
   if (C % 4 == 0)
-    return stats_pool_ts<float, 4>((const float*)x, N, H, W, C, mean, inv, out, s);
-  return stats_pool_ts<float, 1>((const float*)x, N, H, W, C, mean, inv, out, s);
+    return stats_pool_ts<float, 4>((const float*)x, N, H, W, C, mean, inv, out, in_mean, in_inv, s);
+  return stats_pool_ts<float, 1>((const float*)x, N, H, W, C, mean, inv, out, in_mean, in_inv, s);
 }
 
 // ----------------------------------------------------------------------------
