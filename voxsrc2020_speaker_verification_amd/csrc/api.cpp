@@ -193,6 +193,7 @@ struct Op {
   BneckParams bq{};  // type 12: Cin (cin), C, w (cl.wco), split (S)
   GconvParams gq{};  // type 19
   DpnBlockParams dq{};  // type 31
+  DpnDownParams ddq{};  // type 32
   const float* in_mean = nullptr;  // type 2: input BN+ReLU fused into the pool (DPN68)
   const float* in_inv = nullptr;
   int cin = 0;
@@ -1495,43 +1496,75 @@ static int build_dpn(Builder& B, const float* x, int n, int t, float* out) {
       if (fused) {
         push_block(dq);
       } else {
-        // 1x1a
-        char* A = B.base(S_A, (size_t)n * Hi * Wi * r * es);
-        emit_conv(B, c1, inp, nullptr, 0, 1, 1, 1, 1, 0, 0, Hi, Wi, A, r, 0, nullptr, 0, nullptr, 0,
-                  1 << 30, (const float*)b1.mean->p, (const float*)b1.inv->p);
-        DpnBlockParams da = rest_ok ? block_params(true, A) : DpnBlockParams{};
-        if (rest_ok && dpn_block_ok(da)) {
-          push_block(da);
-          dense += inc;
-          B.tap(S, n, Ho, Wo, bw + dense, ctot);
-          continue;
-        }
-        // grouped 3x3, stride bs, TF SAME (asymmetric for stride 2)
         char* Bb = B.base(S_B, (size_t)n * Ho * Wo * r * es);
-        GconvParams g{};
-        g.x = A; g.ldx = r; g.in_mean = (const float*)b2.mean->p; g.in_inv = (const float*)b2.inv->p;
-        g.w = c2.wgc ? c2.wgc->p : nullptr; g.y = Bb; g.ldy = r;
-        g.N = n; g.H = Hi; g.W = Wi; g.C = r; g.Ho = Ho; g.Wo = Wo; g.gw = c2.cin;
-        g.sh = bs; g.ph = tf_same_beg(Hi, 3, bs); g.pw = tf_same_beg(Wi, 3, bs);
-        if (c2.wgc && !m->no_gconv && c2.cin * c2.groups == r && gconv_ok(g)) {
-          // row segments: enough workgroups to cover the chip a few times over,
-          // each segment >= 4 steps (warm-up window re-read per segment)
-          const int rs = gconv_rs(g);
-          int nseg = 1;
-          while ((long)n * (r / 64) * nseg < 2048 && Ho / (2 * nseg) >= 4 * rs) nseg *= 2;
-          g.seg = (Ho + nseg - 1) / nseg;
-          g.nseg = (Ho + g.seg - 1) / g.seg;
+        // stride-2 projection block: 1x1a at full resolution + grouped 3x3 s2 in
+        // one row-streamed launch (dpnblk.hip), bit-identical to the two below
+        DpnDownParams dd{};
+        bool down = false;
+        if (bs == 2 && !m->no_dpn_block && m->dt == BF16 && c1.wpair && c1.cout == r &&
+            c1.cin == inp.C && c2.wgc && c2.cin <= 16 && c2.cin * c2.groups == r && b1.mean &&
+            b2.mean) {
+          dd.x = inp.p; dd.ldx = inp.ld; dd.cin = inp.C;
+          dd.w1 = c1.wpair->p; dd.kp1 = c1.kp;
+          dd.m1 = (const float*)b1.mean->p; dd.i1 = (const float*)b1.inv->p;
+          dd.wg = c2.wgc->p;
+          dd.m2 = (const float*)b2.mean->p; dd.i2 = (const float*)b2.inv->p;
+          dd.y = Bb; dd.ldy = r; dd.r = r;
+          dd.N = n; dd.H = Hi; dd.W = Wi; dd.Ho = Ho; dd.Wo = Wo;
+          // one workgroup per CU (~130 KB LDS) per (segment, 128-channel slice)
+          int nseg = m->dpn_nseg > 0 ? m->dpn_nseg : 1;
+          if (m->dpn_nseg <= 0)
+            while ((long)n * nseg * (r / 128) < m->num_cu && Ho / (2 * nseg) >= 8) nseg *= 2;
+          dd.seg = (Ho + nseg - 1) / nseg;
+          dd.nseg = (Ho + dd.seg - 1) / dd.seg;
+          down = dpn_down_ok(dd) != 0;
+        }
+        if (down) {
           Op op;
           op.kind = OP_CONV;
-          op.type = 19;
-          op.gq = g;
-          op.flops = 2.0 * n * Ho * Wo * (double)r * 9.0 * c2.cin;
-          op.bytes = es * ((double)n * Hi * Wi * r + (double)n * Ho * Wo * r);
+          op.type = 32;
+          op.ddq = dd;
+          op.flops = 2.0 * n * ((double)Hi * Wi * c1.cin * r + (double)Ho * Wo * r * 9.0 * c2.cin);
+          op.bytes = es * ((double)n * Hi * Wi * inp.C + (double)n * Ho * Wo * r);
           B.ops->push_back(op);
         } else {
-          emit_conv(B, c2, Act{A, r, n, Hi, Wi, r}, nullptr, 0, bs, bs, 1, 1, tf_same_beg(Hi, 3, bs),
-                    tf_same_beg(Wi, 3, bs), Ho, Wo, Bb, r, 0, nullptr, 0, nullptr, 0, 1 << 30,
-                    (const float*)b2.mean->p, (const float*)b2.inv->p);
+          // 1x1a
+          char* A = B.base(S_A, (size_t)n * Hi * Wi * r * es);
+          emit_conv(B, c1, inp, nullptr, 0, 1, 1, 1, 1, 0, 0, Hi, Wi, A, r, 0, nullptr, 0, nullptr, 0,
+                    1 << 30, (const float*)b1.mean->p, (const float*)b1.inv->p);
+          DpnBlockParams da = rest_ok ? block_params(true, A) : DpnBlockParams{};
+          if (rest_ok && dpn_block_ok(da)) {
+            push_block(da);
+            dense += inc;
+            B.tap(S, n, Ho, Wo, bw + dense, ctot);
+            continue;
+          }
+          // grouped 3x3, stride bs, TF SAME (asymmetric for stride 2)
+          GconvParams g{};
+          g.x = A; g.ldx = r; g.in_mean = (const float*)b2.mean->p; g.in_inv = (const float*)b2.inv->p;
+          g.w = c2.wgc ? c2.wgc->p : nullptr; g.y = Bb; g.ldy = r;
+          g.N = n; g.H = Hi; g.W = Wi; g.C = r; g.Ho = Ho; g.Wo = Wo; g.gw = c2.cin;
+          g.sh = bs; g.ph = tf_same_beg(Hi, 3, bs); g.pw = tf_same_beg(Wi, 3, bs);
+          if (c2.wgc && !m->no_gconv && c2.cin * c2.groups == r && gconv_ok(g)) {
+            // row segments: enough workgroups to cover the chip a few times over,
+            // each segment >= 4 steps (warm-up window re-read per segment)
+            const int rs = gconv_rs(g);
+            int nseg = 1;
+            while ((long)n * (r / 64) * nseg < 2048 && Ho / (2 * nseg) >= 4 * rs) nseg *= 2;
+            g.seg = (Ho + nseg - 1) / nseg;
+            g.nseg = (Ho + g.seg - 1) / g.seg;
+            Op op;
+            op.kind = OP_CONV;
+            op.type = 19;
+            op.gq = g;
+            op.flops = 2.0 * n * Ho * Wo * (double)r * 9.0 * c2.cin;
+            op.bytes = es * ((double)n * Hi * Wi * r + (double)n * Ho * Wo * r);
+            B.ops->push_back(op);
+          } else {
+            emit_conv(B, c2, Act{A, r, n, Hi, Wi, r}, nullptr, 0, bs, bs, 1, 1, tf_same_beg(Hi, 3, bs),
+                      tf_same_beg(Wi, 3, bs), Ho, Wo, Bb, r, 0, nullptr, 0, nullptr, 0, 1 << 30,
+                      (const float*)b2.mean->p, (const float*)b2.inv->p);
+          }
         }
         // 1x1c -> [res add in place | new dense channels appended]
         emit_conv(B, c3, Act{Bb, r, n, Ho, Wo, r}, nullptr, 0, 1, 1, 1, 1, 0, 0, Ho, Wo, S, ctot,
@@ -1632,6 +1665,7 @@ static hipError_t run_op(vox_model* m, const Op& op, hipStream_t s) {
     case 25: return launch_conv3_rw(op.cp, m->num_cu, s);
     case 30: return launch_conv3_ks(op.cp, m->num_cu, s);
     case 31: return launch_dpn_block(op.dq, s);
+    case 32: return launch_dpn_down(op.ddq, s);
     case 26: return launch_conv3_utt(op.cp, m->num_cu, s);
     case 27: return launch_conv1x1_smallk(op.cp, s);
     case 29: return launch_conv1x1_nw(op.cp, m->num_cu, s);
@@ -1905,6 +1939,8 @@ extern "C" int vox_profile(vox_model* m, const float* d_x, int n, int t, int f, 
         tag |= (1 << 29) | (1 << 18) | (1 << 16);
       else if (o.type == 31)
         tag |= (1 << 28) | (1 << 19);
+      else if (o.type == 32)
+        tag |= (1 << 28) | (1 << 18);
       else if (o.type == 8)
         tag |= (o.cl.wco << 4) | (o.cl.wpx << 8) | (((o.cp.cinp + 31) / 32) << 16) | (1 << 20);
       else if (o.type == 0 || o.type == 5)
@@ -1943,7 +1979,7 @@ extern "C" int vox_plan_describe(vox_model* m, const float* d_x, int n, int t, i
                              "win", "rr", "gemm", "chain", "stem", "bneck", "chainrows", "splits2",
                              "cvt16", "atttanh", "attpool", "gemmpipe", "gconv", "conv3pipe",
                              "gemmwide", "s2fused", "-", "chainfused", "conv3rw", "conv3utt",
-                             "smallk", "conv3s2r", "nw", "conv3ks", "dpnblock"};
+                             "smallk", "conv3s2r", "nw", "conv3ks", "dpnblock", "dpndown"};
   for (const Op& o : m->plan) {
     char line[256];
     const ConvParams& p = o.cp;
@@ -1960,6 +1996,10 @@ extern "C" int vox_plan_describe(vox_model* m, const float* d_x, int n, int t, i
       std::snprintf(line, sizeof(line), "bneck N=%d H=%d W=%d Cin=%d C=%d w=%d split=%d seg=%d nseg=%d flops=%.4g bytes=%.4g\n",
                     o.bq.N, o.bq.H, o.bq.W, o.cin, o.C, o.cl.wco, o.S, o.bq.seg, o.bq.nseg, o.flops,
                     o.bytes);
+    else if (o.type == 32)
+      std::snprintf(line, sizeof(line), "dpndown N=%d H=%d W=%d Cin=%d r=%d Ho=%d Wo=%d seg=%d nseg=%d flops=%.4g bytes=%.4g\n",
+                    o.ddq.N, o.ddq.H, o.ddq.W, o.ddq.cin, o.ddq.r, o.ddq.Ho, o.ddq.Wo, o.ddq.seg,
+                    o.ddq.nseg, o.flops, o.bytes);
     else if (o.type == 31)
       std::snprintf(line, sizeof(line), "dpnblock N=%d H=%d W=%d Cin=%d Cout=%d bw=%d from_a=%d seg=%d nseg=%d flops=%.4g bytes=%.4g\n",
                     o.dq.N, o.dq.H, o.dq.W, o.dq.cin, o.dq.cout, o.dq.bw, o.dq.from_a, o.dq.seg, o.dq.nseg,

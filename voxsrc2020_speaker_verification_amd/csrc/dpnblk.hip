@@ -531,6 +531,286 @@ __global__ __launch_bounds__(DB_THREADS) void dpn_block_rows(DpnBlockParams p) {
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// Projection block front of a stride-2 stage (dpn_model.py:57-87 with
+// stride 2; stage 2 of DPN68): the 1x1a (cin -> r, BN+ReLU prologue) at the
+// full input resolution and the grouped 3x3 with stride 2 (TF SAME, pad_beg 0)
+// in one row-streamed launch.  Unfused, the 1x1a writes its r-channel map at
+// full resolution (1.57 GB at B = 64, 80 x 600) and the 3x3 reads it back.
+// Workgroup = (utterance segment of output rows, 128-channel slice of r; the
+// groups lie inside a slice).  Step = output row o: the 1x1a of input rows
+// 2o+1 and 2o+2 (waves 0-3 / 4-7, one 32-cout pair each) into a 3-row ring
+// (row 2o stays from the previous step; segments share one input row and
+// recompute it, nothing is written in place), then the 3x3 of row o to HBM.
+// Bit-identical to gemm1x1_ws<.., GS_PRO> -> gconv3x3_rows<.., 2, ..>: the
+// 1x1a prologue and K order, the bf16 1x1a output, the 3x3's staging
+// prologue, its stride-2 column-slot layout and tap pairing.
+namespace {
+constexpr int DD_KS = 5;     // 1x1a k-steps (cin <= 160)
+constexpr int DD_PXS = 22;   // X1 units per pixel (20 + 2; 22 = 6 mod 16: conflict-free b128 reads)
+constexpr int DD_TPI = 5;    // input 16-pixel tiles per row (65 <= W <= 80)
+constexpr int DD_TPO = 3;    // output tiles per row (Wo = 40)
+struct DdGeo {
+  int spw, rowb, zero, x1, tb, lds;
+};
+__host__ __device__ inline DdGeo dd_geo(int W) {
+  DdGeo g{};
+  int spw = 2 * (W + 2);
+  spw += ((2 - spw) % 16 + 16) % 16;
+  g.spw = spw;
+  g.rowb = 8 * spw * 16;
+  g.zero = 3 * g.rowb;
+  g.x1 = g.zero + 512 * DD_TPO + 1024;
+  g.tb = g.x1 + 2 * 16 * DD_TPI * DD_PXS * 16;   // m1 i1 (160 each) -m2 i2 (128 each)
+  g.lds = g.tb + (2 * 32 * DD_KS + 2 * DB_R) * 4;
+  return g;
+}
+}  // namespace
+
+__global__ __launch_bounds__(DB_THREADS) void dpn_down_rows(DpnDownParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int KW = 32 * DD_KS;                 // padded K of the 1x1a
+  constexpr int UP = (16 * DD_TPI + 24) / 25;    // pixels per staging thread per row (80 / 25)
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int col = lane & 15, g = lane >> 4;
+  const int W = p.W, H = p.H, Ho = p.Ho, Wo = p.Wo;
+  const DdGeo geo = dd_geo(W);
+  const int SPW = geo.spw, ROWB = geo.rowb;
+  const int E = (W + 3) >> 1;                    // even padded columns come first
+  auto slot_of = [&](int xp) { return (xp & 1) ? E + (xp >> 1) : (xp >> 1); };
+  // blockIdx -> (segment id, slice): the slices of a segment 8 apart (one XCD,
+  // one L2 for their shared input rows)
+  const int b = blockIdx.x;
+  const int nsl = p.r / DB_R;
+  const int sid = (b >> 3) / nsl * 8 + (b & 7), slice = (b >> 3) % nsl;
+  const int n = sid / p.nseg;
+  if (n >= p.N) return;
+  const int s0 = (sid - n * p.nseg) * p.seg;
+  const int s1 = min(s0 + p.seg, Ho);
+  if (s0 >= s1) return;
+  const int c0 = slice * DB_R;
+  const size_t rowe = (size_t)W * p.ldx;
+  const bf16_t* __restrict__ Xn = reinterpret_cast<const bf16_t*>(p.x) + (size_t)n * H * rowe;
+
+  // ---- BN tables
+  float* tb = reinterpret_cast<float*>(smem + geo.tb);
+  for (int c = tid; c < KW; c += DB_THREADS) {
+    tb[c] = c < p.cin ? p.m1[c] : 0.f;
+    tb[KW + c] = c < p.cin ? p.i1[c] : 0.f;
+  }
+  for (int c = tid; c < DB_R; c += DB_THREADS) {
+    tb[2 * KW + c] = -p.m2[c0 + c];
+    tb[2 * KW + DB_R + c] = p.i2[c0 + c];
+  }
+  // zero the pad column slots of the ring rows, and the zero line
+  for (int u = tid; u < 3 * 8 * 4; u += DB_THREADS) {
+    const int row = u >> 5, sp = (u >> 2) & 7, e = u & 3;
+    const int xs = slot_of((e >> 1) ? W + 1 : 0);
+    *reinterpret_cast<uint4*>(smem + row * ROWB + (sp * SPW + 2 * xs + (e & 1)) * 16) = uint4{0u, 0u, 0u, 0u};
+  }
+  for (int u = tid; u < 32 * DD_TPO; u += DB_THREADS)
+    *reinterpret_cast<uint4*>(smem + geo.zero + u * 16) = uint4{0u, 0u, 0u, 0u};
+  __syncthreads();
+
+  // ---- staging roles: thread t < 500 -> chunk t % 20 (8 channels) of pixels
+  // t / 20 + 25 j, both rows of a step
+  const bool sact = tid < 500;
+  const int sch = tid % 20, spl = tid / 20;
+  const bool cval = sact && 8 * sch < p.cin;
+  const uint4* zl = g_db_zero;
+  // rows ra, ra + 1 (each only if < H and < rlim)
+  auto load_rows = [&](int ra, int rlim, uint4 (&v)[2][UP]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int r = ra + k;
+      const bf16_t* __restrict__ Xr = Xn + (size_t)r * rowe;
+#pragma unroll
+      for (int j = 0; j < UP; ++j) {
+        const int px = spl + 25 * j;
+        const bool ok = cval && px < W && r < H && r < rlim;
+        v[k][j] = *(ok ? reinterpret_cast<const uint4*>(Xr + (size_t)px * p.ldx + 8 * sch) : zl);
+      }
+    }
+  };
+  auto stage = [&](const uint4 (&v)[2][UP]) __attribute__((always_inline)) {
+    if (!sact) return;
+    float pm[8], pi[8];
+    *reinterpret_cast<f32x4*>(pm) = *reinterpret_cast<const f32x4*>(tb + 8 * sch);
+    *reinterpret_cast<f32x4*>(pm + 4) = *reinterpret_cast<const f32x4*>(tb + 8 * sch + 4);
+    *reinterpret_cast<f32x4*>(pi) = *reinterpret_cast<const f32x4*>(tb + KW + 8 * sch);
+    *reinterpret_cast<f32x4*>(pi + 4) = *reinterpret_cast<const f32x4*>(tb + KW + 8 * sch + 4);
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+      for (int j = 0; j < UP; ++j) {
+        const int px = spl + 25 * j;
+        if (px >= W) continue;
+        const bf16x8 bv = __builtin_bit_cast(bf16x8, v[k][j]);
+        bf16x8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = (bf16_t)fmaxf(((float)bv[e] - pm[e]) * pi[e], 0.f);
+        *reinterpret_cast<bf16x8*>(smem + geo.x1 + ((k * 16 * DD_TPI + px) * DD_PXS + sch) * 16) = o;
+      }
+  };
+
+  // ---- 1x1a: wave -> (row k = wave / 4 of the step, couts pair q1 = wave % 4 of the slice)
+  const int q1 = wave & 3, kr = wave >> 2;
+  bf16x8 a1[2][DD_KS];
+  {
+    const bf16_t* w1 = reinterpret_cast<const bf16_t*>(p.w1);
+    const int q = c0 / 32 + q1;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int s = 0; s < DD_KS; ++s) {
+        const int c = 32 * s + 8 * g;
+        a1[u][s] = c < p.kp1 ? ld16(w1 + (size_t)((2 * q + u) * 16 + col) * p.kp1 + c) : bf16x8{};
+      }
+  }
+  const int h1u = ((4 * q1 + g) >> 1) * SPW + ((4 * q1 + g) & 1);
+  auto ring_off = [&](int r) { return ((r - 2 * s0 + 3) % 3) * ROWB; };   // input row r >= 2 s0
+  // input row r (waves of row part kr) -> its ring slot; zeros for r >= H
+  auto gemm1a = [&](int r) __attribute__((always_inline)) {
+    const int slot = ring_off(r);
+    if (r >= H) {
+#pragma unroll
+      for (int t = 0; t < DD_TPI; ++t) {
+        const int px = 16 * t + col;
+        if (px < W)
+          *reinterpret_cast<uint4*>(smem + slot + (h1u + 2 * slot_of(px + 1)) * 16) = uint4{0u, 0u, 0u, 0u};
+      }
+      return;
+    }
+    f32x4 acc[2][DD_TPI];
+#pragma unroll
+    for (int t = 0; t < DD_TPI; ++t) acc[0][t] = acc[1][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < DD_KS; ++s)
+#pragma unroll
+      for (int t = 0; t < DD_TPI; ++t) {
+        const bf16x8 bv = *reinterpret_cast<const bf16x8*>(
+            smem + geo.x1 + ((kr * 16 * DD_TPI + 16 * t + col) * DD_PXS + 4 * s + g) * 16);
+        acc[0][t] = mfma_step(a1[0][s], bv, acc[0][t]);
+        acc[1][t] = mfma_step(a1[1][s], bv, acc[1][t]);
+      }
+    float nm2[8], iv2[8];
+    {
+      const float* t2 = tb + 2 * KW + 32 * q1 + 8 * g;
+      *reinterpret_cast<f32x4*>(nm2) = *reinterpret_cast<const f32x4*>(t2);
+      *reinterpret_cast<f32x4*>(nm2 + 4) = *reinterpret_cast<const f32x4*>(t2 + 4);
+      *reinterpret_cast<f32x4*>(iv2) = *reinterpret_cast<const f32x4*>(t2 + DB_R);
+      *reinterpret_cast<f32x4*>(iv2 + 4) = *reinterpret_cast<const f32x4*>(t2 + DB_R + 4);
+    }
+#pragma unroll
+    for (int t = 0; t < DD_TPI; ++t) {
+      const int px = 16 * t + col;
+      if (px >= W) continue;
+      typedef float f32x2 __attribute__((ext_vector_type(2)));
+      bf16x8 rr;
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        const int e0 = 2 * h, e1 = 2 * h + 1;
+        const float v0 = (float)(bf16_t)(e0 < 4 ? acc[0][t][e0] : acc[1][t][e0 - 4]);
+        const float v1 = (float)(bf16_t)(e1 < 4 ? acc[0][t][e1] : acc[1][t][e1 - 4]);
+        f32x2 xv = {v0, v1};
+        const f32x2 m2 = {nm2[e0], nm2[e1]};
+        const f32x2 i2 = {iv2[e0], iv2[e1]};
+        xv = (xv + m2) * i2;
+        rr[e0] = (bf16_t)xv[0];
+        rr[e1] = (bf16_t)xv[1];
+      }
+      *reinterpret_cast<bf16x8*>(smem + slot + (h1u + 2 * slot_of(px + 1)) * 16) = relu_bf16(rr);
+    }
+  };
+
+  // ---- grouped 3x3 stride 2: slab `wave` of the slice (channels c0 + 16 wave + 4 g + 0..3)
+  bf16x8 ag[5];
+  {
+    const bf16_t* wp = reinterpret_cast<const bf16_t*>(p.wg) + ((size_t)(c0 / 16 + wave) * 5 * 64 + lane) * 8;
+#pragma unroll
+    for (int m = 0; m < 5; ++m) ag[m] = ld16(wp + m * 512);
+  }
+  int lofs[5];
+#pragma unroll
+  for (int m = 0; m < 5; ++m) {
+    const int tap = 2 * m + (g >> 1);
+    const int kx = (tap < 9 ? tap : 8) % 3;
+    const int chunk = 2 * wave + (g & 1);
+    lofs[m] = ((chunk >> 1) * SPW + 2 * slot_of(2 * col + kx + 1) + (chunk & 1)) * 16;
+  }
+  bf16_t* __restrict__ Y = reinterpret_cast<bf16_t*>(p.y) + (size_t)n * Ho * Wo * p.ldy + c0 + 16 * wave + 4 * g;
+  auto gconv_row = [&](int o) __attribute__((always_inline)) {
+    const int r0 = __builtin_amdgcn_readfirstlane(ring_off(2 * o));
+    const int r1 = __builtin_amdgcn_readfirstlane(ring_off(2 * o + 1));
+    const int r2 = __builtin_amdgcn_readfirstlane(ring_off(2 * o + 2));
+    f32x4 acc[DD_TPO];
+#pragma unroll
+    for (int t = 0; t < DD_TPO; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int m = 0; m < 5; ++m) {
+      int addr;
+      if (m == 0) addr = r0 + lofs[0];
+      else if (m == 1) addr = ((g >> 1) ? r1 : r0) + lofs[1];
+      else if (m == 2) addr = r1 + lofs[2];
+      else if (m == 3) addr = r2 + lofs[3];
+      else addr = (g >> 1) ? geo.zero : r2 + lofs[4];
+#pragma unroll
+      for (int t = 0; t < DD_TPO; ++t) {
+        const bf16x8 bv = *reinterpret_cast<const bf16x8*>(smem + addr + 512 * t);
+        acc[t] = mfma_step(ag[m], bv, acc[t]);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < DD_TPO; ++t) {
+      const int oc = 16 * t + col;
+      bf16x4 o4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o4[e] = (bf16_t)acc[t][e];
+      void* d = oc < Wo ? (void*)(Y + ((size_t)o * Wo + oc) * p.ldy) : (void*)&g_db_sink[lane];
+      *reinterpret_cast<bf16x4*>(d) = o4;
+    }
+  };
+
+  // ---- prologue: input row 2 s0 (the first window row) into the ring
+  const int rlim = 2 * s1 + 1;   // input rows this segment needs: [2 s0, 2 s1]
+  uint4 pf[2][UP];               // one step ahead
+  load_rows(2 * s0, 2 * s0 + 1, pf);             // row 2 s0 only
+  stage(pf);
+  load_rows(2 * s0 + 1, rlim, pf);               // step s0: rows 2 s0 + 1, 2 s0 + 2
+  __syncthreads();
+  if (kr == 0) gemm1a(2 * s0);
+  __syncthreads();
+  for (int o = s0; o < s1; ++o) {
+    // X1 is free: the previous step's 1x1a finished before its second barrier
+    stage(pf);         // rows 2o+1, 2o+2
+    if (o + 1 < s1) load_rows(2 * o + 3, rlim, pf);
+    __syncthreads();   // X1 = rows 2o+1, 2o+2; ring slots of rows 2o-2, 2o-1 free (3x3 of o-1 done)
+    gemm1a(2 * o + 1 + kr);
+    __syncthreads();   // ring rows 2o .. 2o+2 complete
+    gconv_row(o);
+  }
+}
+
+int dpn_down_ok(const DpnDownParams& p) {
+  return p.W > 16 * (DD_TPI - 1) && p.W <= 16 * DD_TPI && p.Wo == (p.W + 1) / 2 && p.Wo <= 16 * DD_TPO &&
+         p.Ho == (p.H + 1) / 2 && p.H % 2 == 0 && p.W % 2 == 0 &&   // TF SAME stride 2: pad_beg 0
+         p.cin > 0 && p.cin <= 32 * DD_KS && p.cin % 8 == 0 && p.cin <= p.ldx && p.ldx % 8 == 0 &&
+         p.kp1 >= p.cin && p.kp1 <= 32 * DD_KS && p.r % DB_R == 0 && p.ldy % 4 == 0 && p.N > 0 &&
+         p.seg > 0 && p.nseg > 0 && (long)p.seg * p.nseg >= p.Ho;
+}
+
+hipError_t launch_dpn_down(const DpnDownParams& p, hipStream_t s) {
+  if (!dpn_down_ok(p) || !p.x || !p.y || !p.w1 || !p.m1 || !p.i1 || !p.wg || !p.m2 || !p.i2)
+    return hipErrorInvalidValue;
+  const int segs = p.N * p.nseg;
+  const int nsl = p.r / DB_R;
+  const dim3 grid((segs + 7) / 8 * 8 * nsl);
+  hipLaunchKernelGGL(dpn_down_rows, grid, dim3(DB_THREADS), dd_geo(p.W).lds, s, p);
+  return hipGetLastError();
+}
+
 int dpn_block_ok(const DpnBlockParams& p) {
   return p.W > 16 * (DB_TPR - 1) && p.W <= 16 * DB_TPR && p.cin > 0 && p.cin <= 128 &&
          p.cin % 8 == 0 && p.cin <= p.ldx && p.kp3 == DB_R &&

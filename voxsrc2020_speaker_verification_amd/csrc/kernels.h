@@ -229,6 +229,19 @@ struct DpnBlockParams {
   int dbg;   // diagnostics (VOXEMB_DPN_DBG, VOX_DIAG builds): 256 = clock stamps
 };
 hipError_t dpn_trace_read(void* dst, size_t bytes);
+// Projection block front of a stride-2 DPN stage (dpnblk.hip): 1x1a (cin ->
+// r, prologue m1/i1, paired-row weights) at the input resolution + grouped
+// 3x3 stride 2 (gconv3x3_rows' weights, gw <= 16, prologue m2/i2) -> y (bf16,
+// r channels, ld ldy) at Ho x Wo.  65 <= W <= 80, even H and W, cin <= 160.
+struct DpnDownParams {
+  const void* x; int ldx; int cin;
+  const void* w1; int kp1; const float* m1; const float* i1;
+  const void* wg; const float* m2; const float* i2;
+  void* y; int ldy; int r;
+  int N, H, W, Ho, Wo, seg, nseg;
+};
+int dpn_down_ok(const DpnDownParams& p);
+hipError_t launch_dpn_down(const DpnDownParams& p, hipStream_t s);
 int dpn_block_ok(const DpnBlockParams& p);
 size_t dpn_block_halo_bytes(const DpnBlockParams& p);
 hipError_t launch_dpn_block(const DpnBlockParams& p, hipStream_t s);
