@@ -363,23 +363,17 @@ __global__ __launch_bounds__(DB_THREADS) void dpn_block_rows(DpnBlockParams p) {
     bf16_t* __restrict__ Y2n = reinterpret_cast<bf16_t*>(p.y2) + (size_t)n * H * W * p.ldy;
     // mode 2: the residual rows (p.res, first bw channels) are prefetched with
     // the ring rows: unit u = tid + 512 i -> (pixel u / 8, chunk u % 8)
-    constexpr int UR = (128 * TPR + DB_THREADS - 1) / DB_THREADS;
     const bf16_t* __restrict__ Rn = reinterpret_cast<const bf16_t*>(p.res) + (size_t)n * H * W * p.ldr;
-    auto load_res = [&](int r, uint4 (&v)[UR]) __attribute__((always_inline)) {
-      const bf16_t* __restrict__ Rr = Rn + (size_t)r * W * p.ldr;
+    // mode 2: the residual (p.res rows, first bw channels) straight into the
+    // 1x1c lanes' registers, requested before the staging of the step
+    uint4 rv[3];
+    auto load_rv = [&](int o) __attribute__((always_inline)) {
+      const bf16_t* __restrict__ Rr = Rn + (size_t)o * W * p.ldr;
 #pragma unroll
-      for (int i = 0; i < UR; ++i) {
-        const int u = tid + DB_THREADS * i, px = u >> 3, c8 = u & 7;
-        const bool ok = px < W && 8 * c8 < p.bw;
-        v[i] = *(ok ? reinterpret_cast<const uint4*>(Rr + (size_t)px * p.ldr + 8 * c8) : zl);
-      }
-    };
-    auto stage_res = [&](const uint4 (&v)[UR], int par) __attribute__((always_inline)) {
-#pragma unroll
-      for (int i = 0; i < UR; ++i) {
-        const int u = tid + DB_THREADS * i, px = u >> 3, c8 = u & 7;
-        if (px < W && 8 * c8 < p.bw)
-          *reinterpret_cast<uint4*>(smem + geo.res + ((par * 16 * TPR + px) * DB_RXS + c8) * 16) = v[i];
+      for (int j = 0; j < 3; ++j) {
+        const int px = 16 * (t3 + j) + col;
+        const bool ok = j < nt3 && px < W && ch3 < p.bw;
+        rv[j] = *(ok ? reinterpret_cast<const uint4*>(Rr + (size_t)px * p.ldr + ch3) : zl);
       }
     };
     auto gemm1c_t = [&](auto NT_, int o) __attribute__((always_inline)) {
@@ -401,9 +395,13 @@ __global__ __launch_bounds__(DB_THREADS) void dpn_block_rows(DpnBlockParams p) {
       for (int j = 0; j < NT; ++j) {
         const int px = 16 * (t3 + j) + col;
         // residual below bw (RES row o), +0.0 on the dense channels (conv1x1_nw)
-        const bf16x8 r = ch3 < p.bw ? *reinterpret_cast<const bf16x8*>(
-                                          smem + geo.res + ((par * 16 * TPR + px) * DB_RXS + (ch3 >> 3)) * 16)
-                                    : bf16x8{};
+        bf16x8 r;
+        if constexpr (FROM_A)
+          r = __builtin_bit_cast(bf16x8, rv[j]);
+        else
+          r = ch3 < p.bw ? *reinterpret_cast<const bf16x8*>(
+                               smem + geo.res + ((par * 16 * TPR + px) * DB_RXS + (ch3 >> 3)) * 16)
+                         : bf16x8{};
         bf16x8 o8;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
@@ -432,11 +430,11 @@ __global__ __launch_bounds__(DB_THREADS) void dpn_block_rows(DpnBlockParams p) {
     using P1 = std::integral_constant<int, 1>;
     if constexpr (FROM_A) {
       // ring rows straight from the (immutable) 1x1a map: rows s0 - 1 .. s1,
-      // zeros outside the image.  Ring row o + 2 and RES row o + 2 are staged
+      // zeros outside the image.  Ring row o + 2 is staged
       // in step o between the 3x3 and the 1x1c (their register prefetch, two
       // rows ahead, has long landed; the wait then covers no fresh stores).
       const int last = min(s1, H - 1);
-      uint4 pf[2][U], rp[2][UR];
+      uint4 pf[2][U];
       if (s0 > 0) {
         load_row(s0 - 1, pf[1]);
         stage_ring(pf[1], ring_off(s0 - 1));
@@ -444,18 +442,12 @@ __global__ __launch_bounds__(DB_THREADS) void dpn_block_rows(DpnBlockParams p) {
         fill_row(ring_off(s0 - 1), -1);
       }
       load_row(s0, pf[0]);
-      load_res(s0, rp[0]);
       if (s0 + 1 <= last) load_row(s0 + 1, pf[1]);
-      if (s0 + 1 < s1) load_res(s0 + 1, rp[1]);
       stage_ring(pf[0], ring_off(s0));
-      stage_res(rp[0], 0);
       if (s0 + 2 <= last) load_row(s0 + 2, pf[0]);
-      if (s0 + 2 < s1) load_res(s0 + 2, rp[0]);
       if (s0 + 1 < H) stage_ring(pf[1], ring_off(s0 + 1));
       else fill_row(ring_off(s0 + 1), -1);
-      if (s0 + 1 < s1) stage_res(rp[1], 1);
       if (s0 + 3 <= last) load_row(s0 + 3, pf[1]);
-      if (s0 + 3 < s1) load_res(s0 + 3, rp[1]);
       __syncthreads();
       auto step = [&](auto PS, int o) __attribute__((always_inline)) {
         constexpr int PI = decltype(PS)::value;
@@ -469,12 +461,9 @@ __global__ __launch_bounds__(DB_THREADS) void dpn_block_rows(DpnBlockParams p) {
             fill_row(ring_off(o + 2), -1);
           }
         }
-        if (o + 2 < s1) {
-          stage_res(rp[PI], (o + 2 - s0) % 3);
-          if (o + 4 < s1) load_res(o + 4, rp[PI]);
-        }
-        gemm1c(o);         // RES row o
-        __syncthreads();   // ring row o + 2, RES row o + 2 staged; H2 free
+        load_rv(o);   // the youngest loads: the 1x1c epilogue's wait covers nothing else
+        gemm1c(o);
+        __syncthreads();   // ring row o + 2 staged; H2 free
       };
       for (int o = s0; o < s1; o += 2) {
         step(P0{}, o);

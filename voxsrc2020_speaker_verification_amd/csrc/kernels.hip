@@ -1351,7 +1351,7 @@ hipError_t launch_splitk_reduce(const float* partial, int S, int M, int coutp, i
 // (bnrelu_k, dpn_model.py:24-29) followed by the pool, without the extra
 // read + write of the map.
 template <typename T, int VN, int TS>
-__global__ __launch_bounds__(64 * TS) void stats_pool_k(const T* __restrict__ x, int N, int H,
+__global__ __launch_bounds__(64 * TS, 4) void stats_pool_k(const T* __restrict__ x, int N, int H,
                                                         int W, int C,
                                                         const float* __restrict__ mean,
                                                         const float* __restrict__ inv,
@@ -1387,7 +1387,9 @@ __global__ __launch_bounds__(64 * TS) void stats_pool_k(const T* __restrict__ x,
   // the first RM rows of this slice stay in registers for the second pass (the
   // re-read was the kernel's second HBM/L2 stream); same summation order
   constexpr int RM = 8;
-  float v[RM][VN];
+  constexpr bool PK = sizeof(T) == 2 && VN == 8;   // rows kept as packed bf16 (exact either way)
+  float v[PK ? 1 : RM][VN];
+  bf16x8 vb[PK ? RM : 1];
   float s[VN];
 #pragma unroll
   for (int e = 0; e < VN; ++e) s[e] = 0.f;
@@ -1397,16 +1399,20 @@ __global__ __launch_bounds__(64 * TS) void stats_pool_k(const T* __restrict__ x,
       const int h = ts + i * TS;
       if (h < H) {
         const T* q = base + (size_t)h * rowstride;
-        if constexpr (sizeof(T) == 2 && VN == 8) {
+        if constexpr (PK) {
           const bf16x8 r = ld16(q);
+          bf16x8 t;
 #pragma unroll
-          for (int e = 0; e < VN; ++e) v[i][e] = elt((float)r[e], e);
+          for (int e = 0; e < VN; ++e) t[e] = (bf16_t)elt((float)r[e], e);
+          vb[i] = t;
+#pragma unroll
+          for (int e = 0; e < VN; ++e) s[e] += (float)t[e];
         } else {
 #pragma unroll
           for (int e = 0; e < VN; ++e) v[i][e] = elt((float)q[e], e);
-        }
 #pragma unroll
-        for (int e = 0; e < VN; ++e) s[e] += v[i][e];
+          for (int e = 0; e < VN; ++e) s[e] += v[i][e];
+        }
       }
     }
     // (unrolled: the loads of 4 rows issue together, the sums keep their order)
@@ -1438,7 +1444,10 @@ __global__ __launch_bounds__(64 * TS) void stats_pool_k(const T* __restrict__ x,
       if (ts + i * TS < H) {
 #pragma unroll
         for (int e = 0; e < VN; ++e) {
-          float d = v[i][e] - mu[e];
+          float x;
+          if constexpr (PK) x = (float)vb[i][e];
+          else x = v[i][e];
+          const float d = x - mu[e];
           s[e] += d * d;
         }
       }
