@@ -43,7 +43,9 @@ def _kernel_name(tag, dt):
             return "conv3x3_s2r" if tag & (1 << 19) else "conv3x3_rw"
         return "conv3x3_pipe"
     if tag & (1 << 28):
-        return "gconv3x3_rows"
+        if tag & (1 << 19):
+            return "dpn_block_rows"
+        return "dpn_down_rows" if tag & (1 << 18) else "gconv3x3_rows"
     if tag & (1 << 27):
         return "gemm1x1_pipe"
     if tag & (1 << 26):

@@ -396,8 +396,9 @@ def test_dpn_block_bitwise_unfused(weights, T, N, nseg, monkeypatch):
     for the projection block the 3x3 + 1x1c after conv1x1_smallk's 1x1a) give
     the same bits as the conv1x1_nw -> gconv3x3_rows -> conv1x1_nw launches,
     every stage-1 tap and the embeddings, for any row segmentation (nseg 0 =
-    the plan's choice; 7 leaves a ragged last segment).  Also covers stage 2's
-    fused projection front (dpn_down_rows) against gemm1x1_ws + gconv3x3_rows."""
+    the plan's choice; 7 leaves a ragged last segment).  Also covers stages 2
+    and 3's fused projection fronts (dpn_down_rows) against gemm1x1_ws +
+    gconv3x3_rows."""
     import torch
     from voxsrc2020_speaker_verification_amd import synth
     spec, t, blob = weights("dpn68", 80)
@@ -414,10 +415,10 @@ def test_dpn_block_bitwise_unfused(weights, T, N, nseg, monkeypatch):
         assert len(lines) == 3 and [("from_a=1" in l) for l in lines] == [True, False, False], lines
         if nseg:
             assert all(f"nseg={nseg}" in l for l in lines), lines
-        # stage 2's projection block front (1x1a at full resolution + grouped
-        # 3x3 stride 2) when its input height is even (TF SAME pad_beg 0)
+        # stages 2 and 3's projection block fronts (1x1a at full resolution +
+        # grouped 3x3 stride 2) where the input height is even (TF SAME pad_beg 0)
         down = [l for l in ex.describe(xd) if l.startswith("dpndown")]
-        assert len(down) == (1 if T % 2 == 0 else 0), down
+        assert len(down) == int(T % 2 == 0) + int(T % 4 == 0), down
     monkeypatch.delenv("VOXEMB_DPN_NSEG", raising=False)
     monkeypatch.setenv("VOXEMB_NO_DPN_BLOCK", "1")
     with _extractor(blob, "bf16") as ex:

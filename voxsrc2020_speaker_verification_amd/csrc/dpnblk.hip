@@ -535,14 +535,23 @@ __global__ __launch_bounds__(DB_THREADS) void dpn_block_rows(DpnBlockParams p) {
 // Bit-identical to gemm1x1_ws<.., GS_PRO> -> gconv3x3_rows<.., 2, ..>: the
 // 1x1a prologue and K order, the bf16 1x1a output, the 3x3's staging
 // prologue, its stride-2 column-slot layout and tap pairing.
+// Shapes (compile time): KS 1x1a k-steps (cin <= 32 KS), TPI / TPO input /
+// output 16-pixel tiles per row, PXS X1 units per pixel (4 KS + 2, = 2 mod 4:
+// conflict-free b128 fragment reads), PL staging pixel lanes (4 KS x PL <= 512
+// threads each own one 8-channel chunk).
+//   stage 2 of DPN68: 80 -> 40 columns, cin 144: <5, 5, 3, 22, 25>
+//   stage 3:          40 -> 20 columns, cin 320: <10, 3, 2, 42, 12>
+template <int KS, int TPI, int TPO, int PXS, int PL>
+struct DdShape {
+  static constexpr int ks = KS, tpi = TPI, tpo = TPO, pxs = PXS, pl = PL;
+};
+using DdS2 = DdShape<5, 5, 3, 22, 25>;
+using DdS3 = DdShape<10, 3, 2, 42, 12>;
 namespace {
-constexpr int DD_KS = 5;     // 1x1a k-steps (cin <= 160)
-constexpr int DD_PXS = 22;   // X1 units per pixel (20 + 2; 22 = 6 mod 16: conflict-free b128 reads)
-constexpr int DD_TPI = 5;    // input 16-pixel tiles per row (65 <= W <= 80)
-constexpr int DD_TPO = 3;    // output tiles per row (Wo = 40)
 struct DdGeo {
   int spw, rowb, zero, x1, tb, lds;
 };
+template <class SH>
 __host__ __device__ inline DdGeo dd_geo(int W) {
   DdGeo g{};
   int spw = 2 * (W + 2);
@@ -550,22 +559,26 @@ __host__ __device__ inline DdGeo dd_geo(int W) {
   g.spw = spw;
   g.rowb = 8 * spw * 16;
   g.zero = 3 * g.rowb;
-  g.x1 = g.zero + 512 * DD_TPO + 1024;
-  g.tb = g.x1 + 2 * 16 * DD_TPI * DD_PXS * 16;   // m1 i1 (160 each) -m2 i2 (128 each)
-  g.lds = g.tb + (2 * 32 * DD_KS + 2 * DB_R) * 4;
+  g.x1 = g.zero + 512 * SH::tpo + 1024;
+  g.tb = g.x1 + 2 * 16 * SH::tpi * SH::pxs * 16;   // m1 i1 (32 KS each) -m2 i2 (128 each)
+  g.lds = g.tb + (2 * 32 * SH::ks + 2 * DB_R) * 4;
   return g;
 }
 }  // namespace
 
+template <class SH>
 __global__ __launch_bounds__(DB_THREADS) void dpn_down_rows(DpnDownParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int DD_KS = SH::ks, DD_TPI = SH::tpi, DD_TPO = SH::tpo, DD_PXS = SH::pxs, PL = SH::pl;
+  constexpr int CPX = 4 * DD_KS;                 // 8-channel chunks per pixel
+  static_assert(CPX * PL <= DB_THREADS, "staging threads");
   constexpr int KW = 32 * DD_KS;                 // padded K of the 1x1a
-  constexpr int UP = (16 * DD_TPI + 24) / 25;    // pixels per staging thread per row (80 / 25)
+  constexpr int UP = (16 * DD_TPI + PL - 1) / PL;   // pixels per staging thread per row
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int col = lane & 15, g = lane >> 4;
   const int W = p.W, H = p.H, Ho = p.Ho, Wo = p.Wo;
-  const DdGeo geo = dd_geo(W);
+  const DdGeo geo = dd_geo<SH>(W);
   const int SPW = geo.spw, ROWB = geo.rowb;
   const int E = (W + 3) >> 1;                    // even padded columns come first
   auto slot_of = [&](int xp) { return (xp & 1) ? E + (xp >> 1) : (xp >> 1); };
@@ -603,10 +616,10 @@ __global__ __launch_bounds__(DB_THREADS) void dpn_down_rows(DpnDownParams p) {
     *reinterpret_cast<uint4*>(smem + geo.zero + u * 16) = uint4{0u, 0u, 0u, 0u};
   __syncthreads();
 
-  // ---- staging roles: thread t < 500 -> chunk t % 20 (8 channels) of pixels
-  // t / 20 + 25 j, both rows of a step
-  const bool sact = tid < 500;
-  const int sch = tid % 20, spl = tid / 20;
+  // ---- staging roles: thread t < CPX PL -> chunk t % CPX (8 channels) of
+  // pixels t / CPX + PL j, both rows of a step
+  const bool sact = tid < CPX * PL;
+  const int sch = tid % CPX, spl = tid / CPX;
   const bool cval = sact && 8 * sch < p.cin;
   const uint4* zl = g_db_zero;
   // rows ra, ra + 1 (each only if < H and < rlim)
@@ -617,7 +630,7 @@ __global__ __launch_bounds__(DB_THREADS) void dpn_down_rows(DpnDownParams p) {
       const bf16_t* __restrict__ Xr = Xn + (size_t)r * rowe;
 #pragma unroll
       for (int j = 0; j < UP; ++j) {
-        const int px = spl + 25 * j;
+        const int px = spl + PL * j;
         const bool ok = cval && px < W && r < H && r < rlim;
         v[k][j] = *(ok ? reinterpret_cast<const uint4*>(Xr + (size_t)px * p.ldx + 8 * sch) : zl);
       }
@@ -634,7 +647,7 @@ __global__ __launch_bounds__(DB_THREADS) void dpn_down_rows(DpnDownParams p) {
     for (int k = 0; k < 2; ++k)
 #pragma unroll
       for (int j = 0; j < UP; ++j) {
-        const int px = spl + 25 * j;
+        const int px = spl + PL * j;
         if (px >= W) continue;
         const bf16x8 bv = __builtin_bit_cast(bf16x8, v[k][j]);
         bf16x8 o;
@@ -782,21 +795,37 @@ __global__ __launch_bounds__(DB_THREADS) void dpn_down_rows(DpnDownParams p) {
   }
 }
 
-int dpn_down_ok(const DpnDownParams& p) {
-  return p.W > 16 * (DD_TPI - 1) && p.W <= 16 * DD_TPI && p.Wo == (p.W + 1) / 2 && p.Wo <= 16 * DD_TPO &&
-         p.Ho == (p.H + 1) / 2 && p.H % 2 == 0 && p.W % 2 == 0 &&   // TF SAME stride 2: pad_beg 0
-         p.cin > 0 && p.cin <= 32 * DD_KS && p.cin % 8 == 0 && p.cin <= p.ldx && p.ldx % 8 == 0 &&
-         p.kp1 >= p.cin && p.kp1 <= 32 * DD_KS && p.r % DB_R == 0 && p.ldy % 4 == 0 && p.N > 0 &&
-         p.seg > 0 && p.nseg > 0 && (long)p.seg * p.nseg >= p.Ho;
+template <class SH>
+static bool dd_fits(const DpnDownParams& p) {
+  return p.W > 16 * (SH::tpi - 1) && p.W <= 16 * SH::tpi && p.Wo <= 16 * SH::tpo &&
+         p.cin <= 32 * SH::ks && p.kp1 <= 32 * SH::ks && p.cin > 32 * SH::ks - 64;
 }
 
+// 0: no instance, 2 / 3: the stage-2 / stage-3 shape
+static int dd_shape(const DpnDownParams& p) {
+  if (!(p.Wo == (p.W + 1) / 2 && p.Ho == (p.H + 1) / 2 && p.H % 2 == 0 && p.W % 2 == 0 &&   // pad_beg 0
+        p.cin > 0 && p.cin % 8 == 0 && p.cin <= p.ldx && p.ldx % 8 == 0 && p.kp1 >= p.cin &&
+        p.r % DB_R == 0 && p.ldy % 4 == 0 && p.N > 0 && p.seg > 0 && p.nseg > 0 &&
+        (long)p.seg * p.nseg >= p.Ho))
+    return 0;
+  if (dd_fits<DdS2>(p)) return 2;
+  if (dd_fits<DdS3>(p)) return 3;
+  return 0;
+}
+
+int dpn_down_ok(const DpnDownParams& p) { return dd_shape(p) != 0; }
+
 hipError_t launch_dpn_down(const DpnDownParams& p, hipStream_t s) {
-  if (!dpn_down_ok(p) || !p.x || !p.y || !p.w1 || !p.m1 || !p.i1 || !p.wg || !p.m2 || !p.i2)
+  const int sh = dd_shape(p);
+  if (!sh || !p.x || !p.y || !p.w1 || !p.m1 || !p.i1 || !p.wg || !p.m2 || !p.i2)
     return hipErrorInvalidValue;
   const int segs = p.N * p.nseg;
   const int nsl = p.r / DB_R;
   const dim3 grid((segs + 7) / 8 * 8 * nsl);
-  hipLaunchKernelGGL(dpn_down_rows, grid, dim3(DB_THREADS), dd_geo(p.W).lds, s, p);
+  if (sh == 2)
+    hipLaunchKernelGGL(dpn_down_rows<DdS2>, grid, dim3(DB_THREADS), dd_geo<DdS2>(p.W).lds, s, p);
+  else
+    hipLaunchKernelGGL(dpn_down_rows<DdS3>, grid, dim3(DB_THREADS), dd_geo<DdS3>(p.W).lds, s, p);
   return hipGetLastError();
 }
 
