@@ -178,13 +178,39 @@ def _host_info():
     return model, os.cpu_count() or 1
 
 
+def _cgroup_cpus():
+    """CPUs the cgroup's CFS quota grants this process (cgroup v2 cpu.max, or
+    v1 cpu.cfs_quota_us / cpu.cfs_period_us), or None when unlimited/unknown.
+    A container can see every core in its affinity set and still be capped
+    to a few CPUs' worth of time: threads beyond the quota only time-slice."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            return max(1, int(q) // int(per))
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        if q > 0:
+            return max(1, q // per)
+    except (OSError, ValueError):
+        pass
+    return None
+
+
 def cpu_baseline(model, feat_dim, T, blob, budget_s=15.0):
     """The C++/OpenMP fp32 restatement of the reference forward
     (oracle/cpu/voxcpu.cpp, the stand-in for tf_extract.py's TF1 CPU
     `sess.run`; kind "port") on a bounded sample of the same workload, on
-    every host core this process may run on (its CPU affinity set,
-    SURVEY §8(d) "all host cores"); OMP_NUM_THREADS and nproc are recorded
-    beside it."""
+    every host core this process may run on: its CPU affinity set (SURVEY
+    §8(d) "all host cores").  A container can see every core of the host in
+    its affinity set and still be capped to a share of them (a cgroup CPU
+    quota, or the share the pool announces through OMP_NUM_THREADS): threads
+    beyond that only time-slice (on the GPU boxes 256 threads under a 16-CPU
+    share ran 6x slower than 16).  So each distinct candidate thread count --
+    the affinity count, the cgroup quota, OMP_NUM_THREADS -- is timed on the
+    sample and the fastest is the baseline; every trial is recorded."""
     from oracle.cpu import CpuModel, build as cpu_build
     from voxsrc2020_speaker_verification_amd import synth
     cpu_build.build()
@@ -194,28 +220,42 @@ def cpu_baseline(model, feat_dim, T, blob, budget_s=15.0):
         affinity = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         affinity = nproc
-    threads = affinity
-    bs = 2 * threads
-    x = synth.make_features(bs, T, feat_dim, seed=99)
-    m.run(x[:2], threads)                       # workspace + weights warm
-    n, t0 = 0, time.perf_counter()
-    while True:
-        m.run(x, threads)
-        n += bs
-        if time.perf_counter() - t0 >= budget_s:
-            break
-    el = time.perf_counter() - t0
-    avx512 = "avx512f" in open("/proc/cpuinfo").read() if os.path.exists("/proc/cpuinfo") else None
+    quota = _cgroup_cpus()
     omp = os.environ.get("OMP_NUM_THREADS")
-    narrow = (f"; the process affinity allows {affinity} of the host's {nproc} cores"
-              if affinity < nproc else "")
-    return {"value": round(n / el, 3), "unit": "utterances/sec", "cores": threads, "kind": "port",
+    cands = {affinity}
+    if quota:
+        cands.add(min(quota, affinity))
+    if omp and omp.isdigit() and int(omp) > 0:
+        cands.add(min(int(omp), affinity))
+    cands = sorted(cands)
+    per = budget_s / len(cands)
+    trials = {}
+    best = None
+    for threads in cands:
+        bs = 2 * threads
+        x = synth.make_features(bs, T, feat_dim, seed=99)
+        m.run(x[:2], threads)                       # workspace + weights warm
+        n, t0 = 0, time.perf_counter()
+        while True:
+            m.run(x, threads)
+            n += bs
+            if time.perf_counter() - t0 >= per:
+                break
+        el = time.perf_counter() - t0
+        trials[str(threads)] = round(n / el, 3)
+        if best is None or n / el > best[0]:
+            best = (n / el, threads, n, el, bs)
+    rate, threads, n, el, bs = best
+    avx512 = "avx512f" in open("/proc/cpuinfo").read() if os.path.exists("/proc/cpuinfo") else None
+    why = (f"fastest of {len(cands)} thread counts tried (affinity {affinity} of {nproc} host cores"
+           + (f", cgroup quota {quota}" if quota else "") + (f", OMP_NUM_THREADS {omp}" if omp else "")
+           + "; " + ", ".join(f"{k} threads {v} utt/s" for k, v in trials.items()) + ")")
+    return {"value": round(rate, 3), "unit": "utterances/sec", "cores": threads, "kind": "port",
             "impl": "cpp_omp", "nproc": nproc, "affinity_cores": affinity,
-            "omp_num_threads_env": omp, "cpu_model": name,
-            "isa": "avx512" if avx512 else "avx2",
+            "cgroup_cpu_quota": quota, "omp_num_threads_env": omp, "trials": trials,
+            "cpu_model": name, "isa": "avx512" if avx512 else "avx2",
             "sample": f"{n} utterances of {T}x{feat_dim} in batches of {bs} ({el:.1f} s; "
-                      f"oracle/cpu/voxcpu.cpp fp32 C++/OpenMP, {threads} threads = every core "
-                      f"in the process affinity set{narrow})"}
+                      f"oracle/cpu/voxcpu.cpp fp32 C++/OpenMP, {threads} threads: {why})"}
 
 
 def main():

@@ -1350,8 +1350,8 @@ hipError_t launch_splitk_reduce(const float* partial, int S, int M, int coutp, i
 // is read, rounded to T: the bits of DPN68's in-place concat_bn_relu pass
 // (bnrelu_k, dpn_model.py:24-29) followed by the pool, without the extra
 // read + write of the map.
-template <typename T, int VN, int TS>
-__global__ __launch_bounds__(64 * TS, 4) void stats_pool_k(const T* __restrict__ x, int N, int H,
+template <typename T, int VN, int TS, bool PRO = false>
+__global__ __launch_bounds__(64 * TS, PRO ? 4 : 1) void stats_pool_k(const T* __restrict__ x, int N, int H,
                                                         int W, int C,
                                                         const float* __restrict__ mean,
                                                         const float* __restrict__ inv,
@@ -1373,7 +1373,7 @@ __global__ __launch_bounds__(64 * TS, 4) void stats_pool_k(const T* __restrict__
   }
   const size_t rowstride = (size_t)W * C;
   const T* base = x + ((size_t)n * H * W + w) * C + (size_t)ch * VN;
-  const bool pro = in_mean != nullptr;
+  constexpr bool pro = PRO;
   float pm[VN], pi[VN];
 #pragma unroll
   for (int e = 0; e < VN; ++e) {
@@ -1675,6 +1675,18 @@ static hipError_t stats_pool_ts(const T* x, int N, int H, int W, int C, const fl
   // order, so it depends on H only -- never on the batch (it used to drop to 4
   // past 2,048 blocks, i.e. a TDNN utterance's pooled bits changed with the
   // batch size past ~680 utterances)
+  if (in_mean) {   // DPN68's concat_bn_relu on the read (time slices as below)
+    if (H >= 64)
+      hipLaunchKernelGGL((stats_pool_k<T, VN, 8, true>), dim3(blocks), dim3(64 * 8), 0, s, x, N, H, W,
+                         C, mean, inv, out, in_mean, in_inv);
+    else if (H >= 16)
+      hipLaunchKernelGGL((stats_pool_k<T, VN, 4, true>), dim3(blocks), dim3(64 * 4), 0, s, x, N, H, W,
+                         C, mean, inv, out, in_mean, in_inv);
+    else
+      hipLaunchKernelGGL((stats_pool_k<T, VN, 1, true>), dim3(blocks), dim3(64), 0, s, x, N, H, W, C,
+                         mean, inv, out, in_mean, in_inv);
+    return hipGetLastError();
+  }
   if (H >= 64) {
     hipLaunchKernelGGL((stats_pool_k<T, VN, 8>), dim3(blocks), dim3(64 * 8), 0, s, x, N, H, W, C,
                        mean, inv, out, in_mean, in_inv);
