@@ -416,9 +416,12 @@ def test_dpn_block_bitwise_unfused(weights, T, N, nseg, monkeypatch):
         if nseg:
             assert all(f"nseg={nseg}" in l for l in lines), lines
         # stages 2 and 3's projection block fronts (1x1a at full resolution +
-        # grouped 3x3 stride 2) where the input height is even (TF SAME pad_beg 0)
+        # grouped 3x3 stride 2) where the input height is even (TF SAME
+        # pad_beg 0), and stage 2's three stride-1 blocks' 1x1a + 3x3
         down = [l for l in ex.describe(xd) if l.startswith("dpndown")]
-        assert len(down) == int(T % 2 == 0) + int(T % 4 == 0), down
+        s2 = [l for l in down if " st=2 " in l]
+        assert len(s2) == int(T % 2 == 0) + int(T % 4 == 0), down
+        assert len(down) - len(s2) == 3, down
     monkeypatch.delenv("VOXEMB_DPN_NSEG", raising=False)
     monkeypatch.setenv("VOXEMB_NO_DPN_BLOCK", "1")
     with _extractor(blob, "bf16") as ex:

@@ -1497,11 +1497,12 @@ static int build_dpn(Builder& B, const float* x, int n, int t, float* out) {
         push_block(dq);
       } else {
         char* Bb = B.base(S_B, (size_t)n * Ho * Wo * r * es);
-        // stride-2 projection block: 1x1a at full resolution + grouped 3x3 s2 in
-        // one row-streamed launch (dpnblk.hip), bit-identical to the two below
+        // 1x1a + grouped 3x3 in one row-streamed launch (dpnblk.hip),
+        // bit-identical to the two below: the stride-2 projection blocks of
+        // stages 2-3 (1x1a at full resolution) and stage 2's stride-1 blocks
         DpnDownParams dd{};
         bool down = false;
-        if (bs == 2 && !m->no_dpn_block && m->dt == BF16 && c1.wpair && c1.cout == r &&
+        if ((bs == 2 || b > 0) && !m->no_dpn_block && m->dt == BF16 && c1.wpair && c1.cout == r &&
             c1.cin == inp.C && c2.wgc && c2.cin <= 16 && c2.cin * c2.groups == r && b1.mean &&
             b2.mean) {
           dd.x = inp.p; dd.ldx = inp.ld; dd.cin = inp.C;
@@ -1510,7 +1511,7 @@ static int build_dpn(Builder& B, const float* x, int n, int t, float* out) {
           dd.wg = c2.wgc->p;
           dd.m2 = (const float*)b2.mean->p; dd.i2 = (const float*)b2.inv->p;
           dd.y = Bb; dd.ldy = r; dd.r = r;
-          dd.N = n; dd.H = Hi; dd.W = Wi; dd.Ho = Ho; dd.Wo = Wo;
+          dd.N = n; dd.H = Hi; dd.W = Wi; dd.Ho = Ho; dd.Wo = Wo; dd.stride = bs;
           // one workgroup per CU (~130 KB LDS) per (segment, 128-channel slice)
           int nseg = m->dpn_nseg > 0 ? m->dpn_nseg : 1;
           if (m->dpn_nseg <= 0)
@@ -1997,9 +1998,9 @@ extern "C" int vox_plan_describe(vox_model* m, const float* d_x, int n, int t, i
                     o.bq.N, o.bq.H, o.bq.W, o.cin, o.C, o.cl.wco, o.S, o.bq.seg, o.bq.nseg, o.flops,
                     o.bytes);
     else if (o.type == 32)
-      std::snprintf(line, sizeof(line), "dpndown N=%d H=%d W=%d Cin=%d r=%d Ho=%d Wo=%d seg=%d nseg=%d flops=%.4g bytes=%.4g\n",
-                    o.ddq.N, o.ddq.H, o.ddq.W, o.ddq.cin, o.ddq.r, o.ddq.Ho, o.ddq.Wo, o.ddq.seg,
-                    o.ddq.nseg, o.flops, o.bytes);
+      std::snprintf(line, sizeof(line), "dpndown N=%d H=%d W=%d Cin=%d r=%d Ho=%d Wo=%d st=%d seg=%d nseg=%d flops=%.4g bytes=%.4g\n",
+                    o.ddq.N, o.ddq.H, o.ddq.W, o.ddq.cin, o.ddq.r, o.ddq.Ho, o.ddq.Wo, o.ddq.stride,
+                    o.ddq.seg, o.ddq.nseg, o.flops, o.bytes);
     else if (o.type == 31)
       std::snprintf(line, sizeof(line), "dpnblock N=%d H=%d W=%d Cin=%d Cout=%d bw=%d from_a=%d seg=%d nseg=%d flops=%.4g bytes=%.4g\n",
                     o.dq.N, o.dq.H, o.dq.W, o.dq.cin, o.dq.cout, o.dq.bw, o.dq.from_a, o.dq.seg, o.dq.nseg,

@@ -541,12 +541,18 @@ __global__ __launch_bounds__(DB_THREADS) void dpn_block_rows(DpnBlockParams p) {
 // threads each own one 8-channel chunk).
 //   stage 2 of DPN68: 80 -> 40 columns, cin 144: <5, 5, 3, 22, 25>
 //   stage 3:          40 -> 20 columns, cin 320: <10, 3, 2, 42, 12>
-template <int KS, int TPI, int TPO, int PXS, int PL>
+//   stage-2 stride-1 blocks (S = 1): 40 columns, cin <= 288: <9, 3, 3, 38, 14, 1>
+// With S = 1 a step adds input rows o+1, o+2 and produces output rows o, o+1
+// (4-row ring; the segment's first window row o-1 is computed by the segment
+// itself: the block's 1x1c writes its output in place only after this launch).
+template <int KS, int TPI, int TPO, int PXS, int PL, int S = 2>
 struct DdShape {
-  static constexpr int ks = KS, tpi = TPI, tpo = TPO, pxs = PXS, pl = PL;
+  static constexpr int ks = KS, tpi = TPI, tpo = TPO, pxs = PXS, pl = PL, st = S;
+  static constexpr int nring = S == 2 ? 3 : 4;
 };
 using DdS2 = DdShape<5, 5, 3, 22, 25>;
 using DdS3 = DdShape<10, 3, 2, 42, 12>;
+using DdF2 = DdShape<9, 3, 3, 38, 14, 1>;
 namespace {
 struct DdGeo {
   int spw, rowb, zero, x1, tb, lds;
@@ -558,7 +564,7 @@ __host__ __device__ inline DdGeo dd_geo(int W) {
   spw += ((2 - spw) % 16 + 16) % 16;
   g.spw = spw;
   g.rowb = 8 * spw * 16;
-  g.zero = 3 * g.rowb;
+  g.zero = SH::nring * g.rowb;
   g.x1 = g.zero + 512 * SH::tpo + 1024;
   g.tb = g.x1 + 2 * 16 * SH::tpi * SH::pxs * 16;   // m1 i1 (32 KS each) -m2 i2 (128 each)
   g.lds = g.tb + (2 * 32 * SH::ks + 2 * DB_R) * 4;
@@ -580,8 +586,9 @@ __global__ __launch_bounds__(DB_THREADS) void dpn_down_rows(DpnDownParams p) {
   const int W = p.W, H = p.H, Ho = p.Ho, Wo = p.Wo;
   const DdGeo geo = dd_geo<SH>(W);
   const int SPW = geo.spw, ROWB = geo.rowb;
-  const int E = (W + 3) >> 1;                    // even padded columns come first
-  auto slot_of = [&](int xp) { return (xp & 1) ? E + (xp >> 1) : (xp >> 1); };
+  constexpr int S = SH::st, NR = SH::nring;
+  const int E = (W + 3) >> 1;                    // stride 2: even padded columns come first
+  auto slot_of = [&](int xp) { return S == 1 ? xp : ((xp & 1) ? E + (xp >> 1) : (xp >> 1)); };
   // blockIdx -> (segment id, slice): the slices of a segment 8 apart (one XCD,
   // one L2 for their shared input rows)
   const int b = blockIdx.x;
@@ -607,7 +614,7 @@ __global__ __launch_bounds__(DB_THREADS) void dpn_down_rows(DpnDownParams p) {
     tb[2 * KW + DB_R + c] = p.i2[c0 + c];
   }
   // zero the pad column slots of the ring rows, and the zero line
-  for (int u = tid; u < 3 * 8 * 4; u += DB_THREADS) {
+  for (int u = tid; u < NR * 8 * 4; u += DB_THREADS) {
     const int row = u >> 5, sp = (u >> 2) & 7, e = u & 3;
     const int xs = slot_of((e >> 1) ? W + 1 : 0);
     *reinterpret_cast<uint4*>(smem + row * ROWB + (sp * SPW + 2 * xs + (e & 1)) * 16) = uint4{0u, 0u, 0u, 0u};
@@ -631,7 +638,7 @@ __global__ __launch_bounds__(DB_THREADS) void dpn_down_rows(DpnDownParams p) {
 #pragma unroll
       for (int j = 0; j < UP; ++j) {
         const int px = spl + PL * j;
-        const bool ok = cval && px < W && r < H && r < rlim;
+        const bool ok = cval && px < W && r >= 0 && r < H && r < rlim;
         v[k][j] = *(ok ? reinterpret_cast<const uint4*>(Xr + (size_t)px * p.ldx + 8 * sch) : zl);
       }
     }
@@ -672,11 +679,13 @@ __global__ __launch_bounds__(DB_THREADS) void dpn_down_rows(DpnDownParams p) {
       }
   }
   const int h1u = ((4 * q1 + g) >> 1) * SPW + ((4 * q1 + g) & 1);
-  auto ring_off = [&](int r) { return ((r - 2 * s0 + 3) % 3) * ROWB; };   // input row r >= 2 s0
-  // input row r (waves of row part kr) -> its ring slot; zeros for r >= H
+  // first input row of the segment's windows: 2 s0 (stride 2, pad_beg 0) or s0 - 1
+  const int rfirst = S == 2 ? 2 * s0 : s0 - 1;
+  auto ring_off = [&](int r) { return ((r - rfirst) % NR) * ROWB; };   // input row r >= rfirst
+  // input row r (waves of row part kr) -> its ring slot; zeros outside the image
   auto gemm1a = [&](int r) __attribute__((always_inline)) {
     const int slot = ring_off(r);
-    if (r >= H) {
+    if (r < 0 || r >= H) {
 #pragma unroll
       for (int t = 0; t < DD_TPI; ++t) {
         const int px = 16 * t + col;
@@ -689,7 +698,8 @@ __global__ __launch_bounds__(DB_THREADS) void dpn_down_rows(DpnDownParams p) {
 #pragma unroll
     for (int t = 0; t < DD_TPI; ++t) acc[0][t] = acc[1][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int s = 0; s < DD_KS; ++s)
+    for (int s = 0; s < DD_KS; ++s) {
+      if (32 * s >= p.kp1) break;   // (uniform) the unfused GEMM's k-steps, no more
 #pragma unroll
       for (int t = 0; t < DD_TPI; ++t) {
         const bf16x8 bv = *reinterpret_cast<const bf16x8*>(
@@ -697,6 +707,7 @@ __global__ __launch_bounds__(DB_THREADS) void dpn_down_rows(DpnDownParams p) {
         acc[0][t] = mfma_step(a1[0][s], bv, acc[0][t]);
         acc[1][t] = mfma_step(a1[1][s], bv, acc[1][t]);
       }
+    }
     float nm2[8], iv2[8];
     {
       const float* t2 = tb + 2 * KW + 32 * q1 + 8 * g;
@@ -740,13 +751,14 @@ __global__ __launch_bounds__(DB_THREADS) void dpn_down_rows(DpnDownParams p) {
     const int tap = 2 * m + (g >> 1);
     const int kx = (tap < 9 ? tap : 8) % 3;
     const int chunk = 2 * wave + (g & 1);
-    lofs[m] = ((chunk >> 1) * SPW + 2 * slot_of(2 * col + kx + 1) + (chunk & 1)) * 16;
+    lofs[m] = ((chunk >> 1) * SPW + 2 * slot_of(S * col + kx + (S == 2 ? 1 : 0)) + (chunk & 1)) * 16;
   }
   bf16_t* __restrict__ Y = reinterpret_cast<bf16_t*>(p.y) + (size_t)n * Ho * Wo * p.ldy + c0 + 16 * wave + 4 * g;
   auto gconv_row = [&](int o) __attribute__((always_inline)) {
-    const int r0 = __builtin_amdgcn_readfirstlane(ring_off(2 * o));
-    const int r1 = __builtin_amdgcn_readfirstlane(ring_off(2 * o + 1));
-    const int r2 = __builtin_amdgcn_readfirstlane(ring_off(2 * o + 2));
+    const int wr = S == 2 ? 2 * o : o - 1;   // window row 0
+    const int r0 = __builtin_amdgcn_readfirstlane(ring_off(wr));
+    const int r1 = __builtin_amdgcn_readfirstlane(ring_off(wr + 1));
+    const int r2 = __builtin_amdgcn_readfirstlane(ring_off(wr + 2));
     f32x4 acc[DD_TPO];
 #pragma unroll
     for (int t = 0; t < DD_TPO; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -775,41 +787,66 @@ __global__ __launch_bounds__(DB_THREADS) void dpn_down_rows(DpnDownParams p) {
     }
   };
 
-  // ---- prologue: input row 2 s0 (the first window row) into the ring
-  const int rlim = 2 * s1 + 1;   // input rows this segment needs: [2 s0, 2 s1]
   uint4 pf[2][UP];               // one step ahead
-  load_rows(2 * s0, 2 * s0 + 1, pf);             // row 2 s0 only
-  stage(pf);
-  load_rows(2 * s0 + 1, rlim, pf);               // step s0: rows 2 s0 + 1, 2 s0 + 2
-  __syncthreads();
-  if (kr == 0) gemm1a(2 * s0);
-  __syncthreads();
-  for (int o = s0; o < s1; ++o) {
-    // X1 is free: the previous step's 1x1a finished before its second barrier
-    stage(pf);         // rows 2o+1, 2o+2
-    if (o + 1 < s1) load_rows(2 * o + 3, rlim, pf);
-    __syncthreads();   // X1 = rows 2o+1, 2o+2; ring slots of rows 2o-2, 2o-1 free (3x3 of o-1 done)
-    gemm1a(2 * o + 1 + kr);
-    __syncthreads();   // ring rows 2o .. 2o+2 complete
-    gconv_row(o);
+  if constexpr (S == 2) {
+    // ---- prologue: input row 2 s0 (the first window row) into the ring
+    const int rlim = 2 * s1 + 1;   // input rows this segment needs: [2 s0, 2 s1]
+    load_rows(2 * s0, 2 * s0 + 1, pf);             // row 2 s0 only
+    stage(pf);
+    load_rows(2 * s0 + 1, rlim, pf);               // step s0: rows 2 s0 + 1, 2 s0 + 2
+    __syncthreads();
+    if (kr == 0) gemm1a(2 * s0);
+    __syncthreads();
+    for (int o = s0; o < s1; ++o) {
+      // X1 is free: the previous step's 1x1a finished before its second barrier
+      stage(pf);         // rows 2o+1, 2o+2
+      if (o + 1 < s1) load_rows(2 * o + 3, rlim, pf);
+      __syncthreads();   // X1 = rows 2o+1, 2o+2; ring slots of rows 2o-2, 2o-1 free (3x3 of o-1 done)
+      gemm1a(2 * o + 1 + kr);
+      __syncthreads();   // ring rows 2o .. 2o+2 complete
+      gconv_row(o);
+    }
+  } else {
+    // ---- prologue: input rows s0 - 1, s0 into the ring
+    const int rlim = s1 + 1;       // input rows this segment needs: [s0 - 1, s1]
+    load_rows(s0 - 1, rlim, pf);
+    stage(pf);
+    load_rows(s0 + 1, rlim, pf);                   // step s0: rows s0 + 1, s0 + 2
+    __syncthreads();
+    gemm1a(s0 - 1 + kr);
+    __syncthreads();
+    for (int o = s0; o < s1; o += 2) {
+      stage(pf);         // rows o+1, o+2
+      if (o + 2 < s1) load_rows(o + 3, rlim, pf);
+      __syncthreads();   // X1 = rows o+1, o+2; ring slots of rows o-3, o-2 free (3x3 of o-2, o-1 done)
+      gemm1a(o + 1 + kr);
+      __syncthreads();   // ring rows o-1 .. o+2 complete
+      gconv_row(o);
+      if (o + 1 < s1) gconv_row(o + 1);
+    }
   }
 }
 
 template <class SH>
-static bool dd_fits(const DpnDownParams& p) {
+static bool dd_fits(const DpnDownParams& p, int cin_lo) {
   return p.W > 16 * (SH::tpi - 1) && p.W <= 16 * SH::tpi && p.Wo <= 16 * SH::tpo &&
-         p.cin <= 32 * SH::ks && p.kp1 <= 32 * SH::ks && p.cin > 32 * SH::ks - 64;
+         p.cin <= 32 * SH::ks && p.kp1 <= 32 * SH::ks && p.cin > cin_lo;
 }
 
-// 0: no instance, 2 / 3: the stage-2 / stage-3 shape
+// 0: no instance; 2 / 3: the stride-2 stage-2 / stage-3 shapes; 1: stride-1 stage 2
 static int dd_shape(const DpnDownParams& p) {
-  if (!(p.Wo == (p.W + 1) / 2 && p.Ho == (p.H + 1) / 2 && p.H % 2 == 0 && p.W % 2 == 0 &&   // pad_beg 0
-        p.cin > 0 && p.cin % 8 == 0 && p.cin <= p.ldx && p.ldx % 8 == 0 && p.kp1 >= p.cin &&
+  if (!(p.cin > 0 && p.cin % 8 == 0 && p.cin <= p.ldx && p.ldx % 8 == 0 && p.kp1 >= p.cin &&
         p.r % DB_R == 0 && p.ldy % 4 == 0 && p.N > 0 && p.seg > 0 && p.nseg > 0 &&
         (long)p.seg * p.nseg >= p.Ho))
     return 0;
-  if (dd_fits<DdS2>(p)) return 2;
-  if (dd_fits<DdS3>(p)) return 3;
+  if (p.stride == 2) {
+    if (!(p.Wo == (p.W + 1) / 2 && p.Ho == (p.H + 1) / 2 && p.H % 2 == 0 && p.W % 2 == 0))  // pad_beg 0
+      return 0;
+    if (dd_fits<DdS2>(p, 96)) return 2;
+    if (dd_fits<DdS3>(p, 256)) return 3;
+    return 0;
+  }
+  if (p.stride == 1 && p.Wo == p.W && p.Ho == p.H && dd_fits<DdF2>(p, 160)) return 1;
   return 0;
 }
 
@@ -824,8 +861,10 @@ hipError_t launch_dpn_down(const DpnDownParams& p, hipStream_t s) {
   const dim3 grid((segs + 7) / 8 * 8 * nsl);
   if (sh == 2)
     hipLaunchKernelGGL(dpn_down_rows<DdS2>, grid, dim3(DB_THREADS), dd_geo<DdS2>(p.W).lds, s, p);
-  else
+  else if (sh == 3)
     hipLaunchKernelGGL(dpn_down_rows<DdS3>, grid, dim3(DB_THREADS), dd_geo<DdS3>(p.W).lds, s, p);
+  else
+    hipLaunchKernelGGL(dpn_down_rows<DdF2>, grid, dim3(DB_THREADS), dd_geo<DdF2>(p.W).lds, s, p);
   return hipGetLastError();
 }
 

@@ -229,16 +229,18 @@ struct DpnBlockParams {
   int dbg;   // diagnostics (VOXEMB_DPN_DBG, VOX_DIAG builds): 256 = clock stamps
 };
 hipError_t dpn_trace_read(void* dst, size_t bytes);
-// Projection block front of a stride-2 DPN stage (dpnblk.hip): 1x1a (cin ->
+// 1x1a + grouped 3x3 of a DPN block in one launch (dpnblk.hip): 1x1a (cin ->
 // r, prologue m1/i1, paired-row weights) at the input resolution + grouped
-// 3x3 stride 2 (gconv3x3_rows' weights, gw <= 16, prologue m2/i2) -> y (bf16,
-// r channels, ld ldy) at Ho x Wo.  65 <= W <= 80, even H and W, cin <= 160.
+// 3x3 (gconv3x3_rows' weights, gw <= 16, prologue m2/i2) -> y (bf16, r
+// channels, ld ldy) at Ho x Wo.  Stride 2 (the projection block of stages 2
+// and 3: W 80 or 40, even H and W) or stride 1 (stage 2: W 40, cin <= 288).
 struct DpnDownParams {
   const void* x; int ldx; int cin;
   const void* w1; int kp1; const float* m1; const float* i1;
   const void* wg; const float* m2; const float* i2;
   void* y; int ldy; int r;
   int N, H, W, Ho, Wo, seg, nseg;
+  int stride;   // 2: the projection block front; 1: a stride-1 block's 1x1a + 3x3 (stage 2)
 };
 int dpn_down_ok(const DpnDownParams& p);
 hipError_t launch_dpn_down(const DpnDownParams& p, hipStream_t s);
