@@ -1556,87 +1556,6 @@ __global__ __launch_bounds__(256) void stats_pool_col(const bf16_t* __restrict__
   *reinterpret_cast<fv*>(o + C) = os;
 }
 
-// Short utterance axis split in two halves: lanes l and l + 32 of a wave hold
-// the same 4-channel column (lane l % 32 = column), rows [0, H2) and [H2, H),
-// so every load instruction reads 2 rows x 256 contiguous bytes.  The two
-// half sums meet with one v_permlane32_swap per value (no LDS), added in the
-// fixed order (first half) + (second half) on both lanes; then the squared
-// deviations the same way (tf.nn.moments' two passes).  Twice
-// stats_pool_col's threads with half its rows each: the grid is ~2.5 rounds of
-// resident waves instead of 1.25.
-template <int HP>
-__global__ __launch_bounds__(256) void stats_pool_h2(const bf16_t* __restrict__ x, int N, int H,
-                                                     int W, int C, const float* __restrict__ mean,
-                                                     const float* __restrict__ inv,
-                                                     float* __restrict__ out) {
-  typedef __bf16 bfv __attribute__((ext_vector_type(4)));
-  typedef unsigned uv __attribute__((ext_vector_type(2)));
-  const int chunks = C / 4;
-  const int lane = threadIdx.x & 63, hh = lane >> 5;
-  const int64_t gcol = ((int64_t)blockIdx.x * 256 + (threadIdx.x & ~63)) / 2 + (lane & 31);
-  const bool valid = gcol < (int64_t)N * W * chunks;
-  const int64_t gc = valid ? gcol : 0;
-  const int n = (int)(gc / ((int64_t)W * chunks));
-  const int r = (int)(gc - (int64_t)n * W * chunks);
-  const int w = r / chunks, ch = r - (r / chunks) * chunks;
-  const int H2 = (H + 1) / 2;
-  const int h0 = hh ? H2 : 0, h1 = hh ? H : H2;
-  const bf16_t* base = x + ((size_t)n * H * W + w) * C + (size_t)ch * 4;
-  const size_t rowstride = (size_t)W * C;
-  uv v[HP];
-#pragma unroll
-  for (int i = 0; i < HP; ++i)
-    if (h0 + i < h1) v[i] = *reinterpret_cast<const uv*>(base + (size_t)(h0 + i) * rowstride);
-  auto both = [&](float a) __attribute__((always_inline)) {
-    // (first half) + (second half), the same fp32 sum on lanes l and l + 32
-    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(a), false, false);
-    const float other = __uint_as_float(hh ? sw[0] : sw[1]);
-    return hh ? other + a : a + other;
-  };
-  float s[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int i = 0; i < HP; ++i)
-    if (h0 + i < h1) {
-      const bfv b = __builtin_bit_cast(bfv, v[i]);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) s[e] += (float)b[e];
-    }
-  float mu[4];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) mu[e] = both(s[e]) / (float)H;
-#pragma unroll
-  for (int i = 0; i < HP; ++i) asm volatile("" : "+v"(v[i]));
-  float q[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int i = 0; i < HP; ++i)
-    if (h0 + i < h1) {
-      const bfv b = __builtin_bit_cast(bfv, v[i]);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float d = (float)b[e] - mu[e];
-        q[e] += d * d;
-      }
-    }
-  float var[4];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) var[e] = both(q[e]) / (float)H;
-  if (!valid) return;
-  float* o = out + (size_t)n * W * 2 * C + (size_t)w * 2 * C + (size_t)ch * 4;
-  // lane l stores the means, lane l + 32 the standard deviations
-  f32x4 res;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const int fm = w * 2 * C + ch * 4 + e, fs = fm + C;
-    float m = mu[e], sd = sqrtf(var[e] + 1e-5f);
-    if (mean) {
-      m = (m - mean[fm]) * inv[fm];
-      sd = (sd - mean[fs]) * inv[fs];
-    }
-    res[e] = hh ? sd : m;
-  }
-  *reinterpret_cast<f32x4*>(o + (hh ? C : 0)) = res;
-}
-
 template <typename T, int VN>
 static hipError_t stats_pool_ts(const T* x, int N, int H, int W, int C, const float* mean,
                                 const float* inv, float* out, const float* in_mean,
@@ -1644,20 +1563,6 @@ static hipError_t stats_pool_ts(const T* x, int N, int H, int W, int C, const fl
   const int64_t cols = (int64_t)N * W * (C / VN);
   if constexpr (sizeof(T) == 2 && VN == 8) {
     if (H <= 32 && !in_mean) {
-#ifdef VOX_DIAG
-      static const int vn8 = [] { const char* e = std::getenv("VOXEMB_POOL_VN8"); return e ? std::atoi(e) : 0; }();
-      if (vn8 && H <= 25 && H > 16) {   // A/B: 8 channels (16-B loads) per thread
-        const unsigned b8 = (unsigned)((cols + 255) / 256);
-        hipLaunchKernelGGL((stats_pool_col<25, 8>), dim3(b8), dim3(256), 0, s, x, N, H, W, C, mean, inv, out);
-        return hipGetLastError();
-      }
-      static const int h2 = [] { const char* e = std::getenv("VOXEMB_POOL_H2"); return e ? std::atoi(e) : 0; }();
-      if (h2) {   // A/B: two row halves per column, lanes l and l + 32
-        const unsigned bh = (unsigned)((cols * 2 * 2 + 255) / 256);
-        hipLaunchKernelGGL((stats_pool_h2<16>), dim3(bh), dim3(256), 0, s, x, N, H, W, C, mean, inv, out);
-        return hipGetLastError();
-      }
-#endif
       // 4 channels (8 B) per thread: the rows of a column in 2 VGPRs each, so
       // the whole utterance axis is in flight at 8 waves per SIMD
       const unsigned b = (unsigned)((cols * 2 + 255) / 256);
