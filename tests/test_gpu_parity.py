@@ -667,6 +667,7 @@ def test_gemm_ws_prologue_bitwise(weights, name, F, T, N, monkeypatch):
     from voxsrc2020_speaker_verification_amd import synth
     spec, t, blob = weights(name, F)
     x = synth.make_features(N, T, F, seed=19)
+    monkeypatch.setenv("VOXEMB_NO_DPN_BLOCK", "1")   # the 1x1a's the fused DPN kernels take
     with _extractor(blob, "bf16") as ex:
         got = ex.run(x)
         pro = [l for l in ex.describe(torch.from_numpy(x).cuda())
