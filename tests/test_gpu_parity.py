@@ -99,6 +99,37 @@ def test_batch_independence_large_batch(weights, precision):
     assert np.array_equal(one[0], full[67])
 
 
+def test_slot_slack_zeroed_over_poisoned_memory(weights):
+    """The TDNN's first-layer taps GEMM (F = 40: cinp 64, K padded to 32-channel
+    steps) reads past the last input row into the slot slack, where zero
+    weights do not help (bf16 NaN x 0 = NaN in the MFMA).  Slots are zeroed
+    whenever they are (re)allocated, so device memory that last held NaN
+    patterns -- handed back to HIP by another user, then reused by a fresh
+    model or by a slot that grows with the batch -- never reaches an output."""
+    import torch
+    from voxsrc2020_speaker_verification_amd import synth
+    spec, t, blob = weights("tdnn", 40)
+    x = synth.make_features(6, 150, 40, seed=37)
+    with _extractor(blob, "bf16") as ex:
+        ref = ex.run(x)
+        ref_small = ex.run(x[:2])
+
+    def poison():
+        junk = torch.full((1 << 28,), float("nan"), dtype=torch.bfloat16, device="cuda")
+        torch.cuda.synchronize()
+        del junk
+        torch.cuda.empty_cache()
+
+    poison()
+    with _extractor(blob, "bf16") as ex:
+        small = ex.run(x[:2])      # slots sized for 2 utterances
+        poison()
+        full = ex.run(x)           # they grow: new allocations
+    assert np.isfinite(small).all() and np.isfinite(full).all()
+    assert np.array_equal(small, ref_small)
+    assert np.array_equal(full, ref)
+
+
 def test_batch_independence_tdnn_pool(weights):
     """TDNN at a batch past 2,048 pooling blocks vs a batch of 10: the plan
     routes every frame layer through the same kernel whatever the batch
