@@ -176,9 +176,24 @@ __global__ __launch_bounds__(CU_NT) void conv3x3_utt(ConvParams p) {
       for (int j = 0; j < CU_PG; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     // taps as a rolled loop (a fully unrolled K loop let the scheduler hoist
-    // reads across k-steps and spill), the 6 k-steps of a tap unrolled
+    // reads across k-steps and spill), the 6 k-steps of a tap unrolled.  The
+    // window (B operand) is fixed for the band, so step s + 1's B fragments are
+    // requested at the end of step s, after its MFMAs (same registers), and
+    // land while the waves meet at the next step's barrier.
+    bf16x8 b[CU_PG];
+    auto read_b = [&](int toff) __attribute__((always_inline)) {
+#pragma unroll
+      for (int j = 0; j < CU_PG; ++j) {
+        int ad = bb[j] + toff;
+        asm volatile("" : "+v"(ad));   // one add per read, nothing precomputed per k-step
+        b[j] = *reinterpret_cast<const bf16x8*>(smem + ad);
+      }
+    };
+    read_b(32 * (-SW - 1));   // tap 0, part 0
     for (int tap = 0; tap < 9; ++tap) {
       const int tsh = 32 * ((tap / 3 - 1) * SW + (tap % 3 - 1));
+      const int tn = tap < 8 ? tap + 1 : tap;   // (the last prefetch is unused)
+      const int tsh_n = 32 * ((tn / 3 - 1) * SW + (tn % 3 - 1));
 #pragma unroll
       for (int part = 0; part < 6; ++part) {
         const int s = tap * 6 + part;
@@ -188,22 +203,16 @@ __global__ __launch_bounds__(CU_NT) void conv3x3_utt(ConvParams p) {
           __syncthreads();   // step s landed for every wave; slot (s+2)%3 released
         }
         if (s + 2 < CU_KS) issue_w(s + 2);
-        const int toff = tsh + part * 2 * SPW * 16;
         const char* L = ring + (s % CU_NST) * CU_WSLOT;
-        bf16x8 a[3], b[CU_PG];
+        bf16x8 a[3];
 #pragma unroll
         for (int i = 0; i < 3; ++i) a[i] = *reinterpret_cast<const bf16x8*>(L + aoff[i]);
-#pragma unroll
-        for (int j = 0; j < CU_PG; ++j) {
-          int ad = bb[j] + toff;
-          asm volatile("" : "+v"(ad));   // one add per read, nothing precomputed per k-step
-          b[j] = *reinterpret_cast<const bf16x8*>(smem + ad);
-        }
 #pragma unroll
         for (int i = 0; i < 3; ++i)
 #pragma unroll
           for (int j = 0; j < CU_PG; ++j) acc[i][j] = mfma_step(a[i], b[j], acc[i][j]);
         __builtin_amdgcn_sched_barrier(0);
+        read_b(part < 5 ? tsh + (part + 1) * 2 * SPW * 16 : tsh_n);   // B of step s + 1
       }
     }
 
