@@ -198,22 +198,42 @@ __global__ __launch_bounds__(CS_NT) void conv3x3_s2r(ConvParams p) {
     f32x4 acc[2];
 #pragma unroll
     for (int jj = 0; jj < 2; ++jj) acc[jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // fragments of k-step s (both pixel tiles); read two steps ahead of their
+    // MFMAs (a 3-set ring, as conv3x3_ks) so the LDS latency hides under the
+    // MFMAs of the two steps before instead of stalling every step.  The six
+    // (pixel tile, chunk part) base addresses are formed once per tile (the
+    // tap offset is an immediate); no inline asm inside the k-loop, which
+    // would split the scheduling region and undo the read-ahead order
+    int ba[2][3];
 #pragma unroll
-    for (int s = 0; s < CS_KS; ++s) {
+    for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+      for (int part = 0; part < 3; ++part) {
+        ba[jj][part] = b * K::BUF + 32 * bslot[jj] + cg[part];
+        asm volatile("" : "+v"(ba[jj][part]));
+      }
+    auto rd = [&](int s, int jj) __attribute__((always_inline)) {
       const int tap = s / 3, part = s % 3;
       const int ky = tap / 3, kx = tap % 3;
       // tap (ky, kx) of output column pc: input column 2pc - 1 + kx ->
       // kx 0: odd slot pc, kx 1: even slot WO + 1 + pc, kx 2: odd slot pc + 1
       const int off = 32 * (ky * SW + (kx == 0 ? 0 : (kx == 1 ? WO + 1 : 1)));
-      bf16x8 bf[2];
+      return *reinterpret_cast<const bf16x8*>(smem + ba[jj][part] + off);
+    };
+    bf16x8 bf[3][2];
 #pragma unroll
-      for (int jj = 0; jj < 2; ++jj) {
-        int a = b * K::BUF + 32 * bslot[jj] + cg[part];
-        asm volatile("" : "+v"(a));
-        bf[jj] = *reinterpret_cast<const bf16x8*>(smem + a + off);
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) bf[s][jj] = rd(s, jj);
+#pragma unroll
+    for (int s = 0; s < CS_KS; ++s) {
+      if (s + 2 < CS_KS) {
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) bf[(s + 2) % 3][jj] = rd(s + 2, jj);
       }
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int jj = 0; jj < 2; ++jj) acc[jj] = mfma_step(wr[s], bf[jj], acc[jj]);
+      for (int jj = 0; jj < 2; ++jj) acc[jj] = mfma_step(wr[s], bf[s % 3][jj], acc[jj]);
       __builtin_amdgcn_sched_barrier(0);
     }
     __syncthreads();   // every thread is done with the staging (store pass tj-1)
