@@ -242,12 +242,12 @@ __global__ __launch_bounds__(KS_NT) void conv3x3_ks(ConvParams p) {
       bf[1] = *reinterpret_cast<const bf16x8*>(smem + bs + off(1));
 #pragma unroll
       for (int s = 0; s < KS_SH; ++s) {
-        if (s + 2 < KS_SH) {
-          bf[(s + 2) % 3] = *reinterpret_cast<const bf16x8*>(smem + bs + off(s + 2));
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        }
+        // hard scheduling fences: with sched_group_barrier hints alone the
+        // compiler issued each read right before its MFMA (lgkmcnt(0) per MFMA)
+        if (s + 2 < KS_SH) bf[(s + 2) % 3] = *reinterpret_cast<const bf16x8*>(smem + bs + off(s + 2));
+        __builtin_amdgcn_sched_barrier(0);
         acc = mfma32(wr[s], bf[s % 3], acc);
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_barrier(0);
       }
       return acc;
     };
