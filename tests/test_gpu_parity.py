@@ -170,7 +170,8 @@ def test_chunk_rule_matches_oracle(weights):
 
 
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
-@pytest.mark.parametrize("shape", [(3, 25, 10, 1024), (2, 200, 1, 1536), (2, 7, 3, 24)])
+@pytest.mark.parametrize("shape", [(3, 25, 10, 1024), (2, 200, 1, 1536), (2, 7, 3, 24),
+                                   (2, 12, 10, 1024), (2, 30, 10, 256)])
 def test_stats_pool_kernel(dtype, shape):
     """models.py:262-269 -- standalone kernel vs the oracle's stats_pool."""
     import ctypes as C

@@ -1580,17 +1580,17 @@ static hipError_t stats_pool_ts(const T* x, int N, int H, int W, int C, const fl
   const int64_t cols = (int64_t)N * W * (C / VN);
   if constexpr (sizeof(T) == 2 && VN == 8) {
     if (H <= 32 && !in_mean) {
-      // 4 channels (8 B) per thread: the rows of a column in 2 VGPRs each, so
-      // the whole utterance axis is in flight at 8 waves per SIMD
       const unsigned b = (unsigned)((cols * 2 + 255) / 256);
+      // 2 channels (4 B) per thread: at the headline (H = 25, T = 200) 2.5 grid
+      // rounds of 8 waves per SIMD instead of 1.25 rounds at 7 (68 VGPRs with 4
+      // channels), 35 -> 31 us in place; <16, 4> had compiled to 248 VGPRs.
+      // Same per-element summation order as 4 channels per thread: same bits
       if (H <= 16)
-        hipLaunchKernelGGL((stats_pool_col<16, 4>), dim3(b), dim3(256), 0, s, x, N, H, W, C, mean, inv, out);
-      else if (H <= 25)   // T = 200 at layer 4 (the headline): 2 channels (4 B) per
-        // thread -- 2.5 grid rounds of 8 waves per SIMD instead of 1.25 rounds
-        // at 7 (68 VGPRs), 35 -> 31 us in place; same per-element order, same bits
+        hipLaunchKernelGGL((stats_pool_col<16, 2>), dim3(2 * b), dim3(256), 0, s, x, N, H, W, C, mean, inv, out);
+      else if (H <= 25)
         hipLaunchKernelGGL((stats_pool_col<25, 2>), dim3(2 * b), dim3(256), 0, s, x, N, H, W, C, mean, inv, out);
       else
-        hipLaunchKernelGGL((stats_pool_col<32, 4>), dim3(b), dim3(256), 0, s, x, N, H, W, C, mean, inv, out);
+        hipLaunchKernelGGL((stats_pool_col<32, 2>), dim3(2 * b), dim3(256), 0, s, x, N, H, W, C, mean, inv, out);
       return hipGetLastError();
     }
   }
