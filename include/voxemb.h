@@ -94,6 +94,14 @@ int vox_profile(vox_model* m, const float* d_x, int n, int t, int f, int reps,
 int vox_plan_describe(vox_model* m, const float* d_x, int n, int t, int f, char* buf,
                       size_t cap);
 
+/* Plan residency counters of the handle: plans built (planned + captured),
+ * calls served by a resident plan without re-planning, plans destroyed
+ * (evicted, or dropped when the workspace grew), and plans resident now
+ * (current + cached; VOXEMB_PLAN_CACHE caps the cached ones, default 16).
+ * Any pointer may be NULL. */
+int vox_plan_stats(const vox_model* m, int64_t* built, int64_t* hits, int64_t* dropped,
+                   int* resident);
+
 /* Standalone stats-pool (+BN) kernel: x NHWC [n,h,w,c] (dtype VOX_FP32 or
  * VOX_BF16), mean/inv per pooled feature (may be NULL = identity),
  * out [n, w*2c] float32 with feature index w*2c + {c | c+C}. */

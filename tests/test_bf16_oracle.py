@@ -196,3 +196,90 @@ def test_headline_plan_b256_matches_small_batches_and_oracle(monkeypatch):
         tot_exact += st["exact"] * st["n"]
         prev = got
     assert tot_exact / tot >= 0.99, tot_exact / tot
+
+
+def _ws_bm(M, cblocks, bn, num_cu=256):
+    """gemm_wide.hip ws_bm: pixels per gemm1x1_ws tile (fewer grid rounds of
+    (bm + bn)-sized work wins; 320-wide tiles are always 128 pixels)."""
+    if bn == 320:
+        return 128
+    big = 192 if bn == 256 else 256
+    cost = lambda bm: (-(-(-(-M // bm) * cblocks) // num_cu)) * (bm + bn)
+    return 128 if cost(128) < cost(big) else big
+
+
+def _dpn_nseg(n, Ho, per_seg_units=1, num_cu=256):
+    """api.cpp build_dpn: row segments of dpn_block_rows / dpn_down_rows."""
+    nseg = 1
+    while n * nseg * per_seg_units < num_cu and Ho // (2 * nseg) >= 8:
+        nseg *= 2
+    return -(-Ho // -(-Ho // nseg))
+
+
+def test_dpn68_bench_plan_b64_matches_small_batches_and_oracle(monkeypatch):
+    """The exact plan `bench.py --model dpn68 --frames 600 --batch 64` times
+    (BASELINE C5: dpn68 80x600, bf16, the bench's weights and rank-0 input;
+    dpn_model.py:57-168).
+    * routing: the fused stage-1 dual-path blocks (dpn_block_rows) and the
+      projection / stage-2 fronts (dpn_down_rows) run with the row segment
+      counts B = 64 picks, and every gemm1x1_ws launch with the tile B = 64
+      picks -- both differ from the B = 2 plans below;
+    * rows [0:2] and [62:64] equal B = 2 runs of the same utterances bit for
+      bit, and the eager launch-by-launch run equals the captured graph;
+    * utterances 0 and 63 pass the per-layer bf16-oracle check
+      (teacher-forced on their rows of every tap)."""
+    import re
+
+    import torch
+    import bench
+    from oracle import models_ref as R
+    from voxsrc2020_speaker_verification_amd.extractor import Extractor
+    name, F, T, B = "dpn68", 80, 600, 64
+    spec, t, blob = bench.bench_weights(name, F)
+    x = bench.bench_features(B, T, F, rank=0)
+    xd = torch.from_numpy(x).cuda()
+    pick = [0, 63]
+    kv = lambda ln: {k: int(v) for k, v in re.findall(r"(\w+)=(-?\d+)", ln)}
+    with Extractor(blob, device=0, precision="bf16") as ex:
+        desc = ex.describe(xd)
+        small = ex.describe(torch.from_numpy(x[:2]).cuda())
+        blk = [kv(ln) for ln in desc if ln.startswith("dpnblock ")]
+        down = [kv(ln) for ln in desc if ln.startswith("dpndown ")]
+        gw = [kv(ln) for ln in desc if ln.startswith("gemmwide ")]
+        assert len(blk) >= 3 and len(down) >= 2 and len(gw) >= 10, desc
+        for d in blk:
+            assert d["N"] == B and d["nseg"] == _dpn_nseg(B, d["H"]), d
+        for d in down:
+            assert d["N"] == B and d["nseg"] == _dpn_nseg(B, d["Ho"], d["r"] // 128), d
+        for g in gw:
+            cb = -(-g["Cout"] // g["bn"])
+            assert g["bm"] == _ws_bm(g["N"] * g["Ho"] * g["Wo"], cb, g["bn"]), g
+        segs = lambda lines: [kv(ln)["nseg"] for ln in lines if ln.startswith(("dpnblock ", "dpndown "))]
+        assert segs(desc) != segs(small)          # the B = 2 plan segments differently
+        taps, emb = ex.layer_outputs(xd, utts=pick)
+        full = ex.run_device(xd)
+        torch.cuda.synchronize()
+        full = full.cpu().numpy()
+        lo, hi = ex.run(x[:2]), ex.run(x[B - 2:])
+    assert np.array_equal(emb, full)
+    assert np.array_equal(lo, full[:2]) and np.array_equal(hi, full[B - 2:])
+    layers = R.layers(spec, t, "bf16")
+    assert len(taps) == len(layers) - 1
+    monkeypatch.setattr(R, "_ACC64", True)
+    prev, tot, tot_exact = x[pick], 0, 0.0
+    for (lname, f), got in zip(layers, taps + [emb[pick]]):
+        ref = f(prev)
+        assert got.shape == ref.shape, (lname, got.shape, ref.shape)
+        if lname == "pool+head":
+            err = float(np.abs(got - ref).max() / np.abs(ref).max())
+            assert err <= 1e-4, (lname, err)
+            break
+        st = compare_bf16(got, ref)
+        print(f"B=64 rows {pick} {lname}: exact {st['exact']:.5f} <=2ulp {st['le2']:.5f} bad {st['bad']:.2e}")
+        assert st["exact"] >= 0.94, (lname, st)
+        assert st["le2"] >= 0.99, (lname, st)
+        assert st["bad"] <= 1e-5, (lname, st)
+        tot += st["n"]
+        tot_exact += st["exact"] * st["n"]
+        prev = got
+    assert tot_exact / tot >= 0.99, tot_exact / tot

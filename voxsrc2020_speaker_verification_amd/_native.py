@@ -49,6 +49,8 @@ _SIGS = [
     ("vox_load_blob", C.c_int, [C.c_void_p, C.c_size_t, C.c_int, C.c_int, C.POINTER(_P)]),
     ("vox_free", None, [_P]),
     ("vox_dim", C.c_int, [_P]),
+    ("vox_plan_stats", C.c_int, [_P, C.POINTER(C.c_int64), C.POINTER(C.c_int64),
+                                 C.POINTER(C.c_int64), C.POINTER(C.c_int)]),
     ("vox_feat_dim", C.c_int, [_P]),
     ("vox_expand_dim", C.c_int, [_P]),
     ("vox_precision", C.c_int, [_P]),

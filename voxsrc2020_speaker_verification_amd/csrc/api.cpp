@@ -210,6 +210,19 @@ struct Tap {
   int n, h, w, c, ld;
 };
 
+// A built plan kept resident (vox_model::cache): its launches, layer taps and
+// captured graph, keyed by the shape and the device pointers it was built for.
+struct PlanEntry {
+  int n = -1, t = -1;
+  const float* x = nullptr;
+  float* out = nullptr;
+  std::vector<Op> plan;
+  std::vector<Tap> taps;
+  hipGraphExec_t exec = nullptr;
+  int uses = 0;
+  uint64_t used = 0;    // LRU stamp
+};
+
 struct vox_model {
   int device = 0;
   DType dt = BF16;
@@ -238,6 +251,21 @@ struct vox_model {
   // (VOXEMB_NO_GRAPH=1: eager launches); rebuilt with the plan
   bool use_graph = true;
   hipGraphExec_t graph_exec = nullptr;
+  // other resident plans (real extraction alternates chunk lengths and ragged
+  // last batches): switching to one swaps it in without re-planning or
+  // re-capturing.  Every plan points into the shared grow-only slots, so a slot
+  // reallocation drops them all.  VOXEMB_PLAN_CACHE = resident plans besides
+  // the current one (default 16, 0 = the single-plan behaviour)
+  std::vector<PlanEntry> cache;
+  int cache_max = 16;
+  // calls of the current plan so far; its graph is captured on call
+  // graph_after + 1 (a shape met once -- one chunk-length bucket of real
+  // extraction -- launches eagerly instead of paying capture + instantiate).
+  // VOXEMB_GRAPH_AFTER, default 1
+  int plan_uses = 0;
+  int graph_after = 1;
+  uint64_t clock = 0;
+  int64_t plans_built = 0, plan_hits = 0, plans_dropped = 0;
   DevBuf stage_in, stage_out;  // host-API staging
   float eps4 = 1.001e-5f, eps2 = 1e-5f;  // BN epsilons (blob header may override)
   // Plan switches: kernel-routing A/B and parity knobs, 0 = the product plan.
@@ -831,7 +859,12 @@ static void emit_conv(Builder& B, const ConvW& cw, Act x, const void* x2, int ld
   if (dt_override == F32) op.type = 5;
   const double es = dt_override == F32 ? 4.0 : (double)es_of(B.m);
   op.flops = 2.0 * M * cw.cout * cw.groups * (double)cw.kh * cw.kw * cw.cin;
-  op.bytes = es * ((double)x.N * x.H * x.W * cw.cin * cw.groups * (x2 ? 2 : 1) +
+  // algorithmic input bytes = the input pixels the conv samples: a kernel
+  // narrower than its stride (the stride-2 1x1 projections,
+  // res2net_model.py:125-127) reads only min(k, s) of every s rows / columns
+  const double rows_in = std::min<double>(x.H, (double)Ho * std::min(cw.kh, sh) + (cw.kh > sh ? cw.kh - sh : 0));
+  const double cols_in = std::min<double>(x.W, (double)Wo * std::min(cw.kw, sw) + (cw.kw > sw ? cw.kw - sw : 0));
+  op.bytes = es * ((double)x.N * rows_in * cols_in * cw.cin * cw.groups * (x2 ? 2 : 1) +
                    (double)M * cw.cout * cw.groups * (res ? 2 : 1));
   B.ops->push_back(op);
 }
@@ -1603,6 +1636,50 @@ static int build_dpn(Builder& B, const float* x, int n, int t, float* out) {
   return VOX_OK;
 }
 
+// destroy every cached plan (after the last launch, which may be one of them)
+static void drop_cache(vox_model* m) {
+  if (m->cache.empty()) return;
+  if (m->done) (void)hipEventSynchronize(m->done);
+  for (PlanEntry& e : m->cache)
+    if (e.exec) (void)hipGraphExecDestroy(e.exec);
+  m->plans_dropped += (int64_t)m->cache.size();
+  m->cache.clear();
+}
+
+// move the current plan into the cache (evicting the least recently used entry)
+static void stash_current(vox_model* m) {
+  if (m->plan_n < 0 || m->cache_max <= 0) {
+    if (m->graph_exec) {
+      if (m->done) (void)hipEventSynchronize(m->done);
+      (void)hipGraphExecDestroy(m->graph_exec);
+      m->graph_exec = nullptr;
+    }
+    m->plan_n = m->plan_t = -1;
+    return;
+  }
+  if ((int)m->cache.size() >= m->cache_max) {
+    size_t lru = 0;
+    for (size_t i = 1; i < m->cache.size(); ++i)
+      if (m->cache[i].used < m->cache[lru].used) lru = i;
+    if (m->cache[lru].exec) {
+      if (m->done) (void)hipEventSynchronize(m->done);
+      (void)hipGraphExecDestroy(m->cache[lru].exec);
+    }
+    ++m->plans_dropped;
+    m->cache.erase(m->cache.begin() + (long)lru);
+  }
+  PlanEntry e;
+  e.n = m->plan_n; e.t = m->plan_t; e.x = m->plan_x; e.out = m->plan_out;
+  e.plan.swap(m->plan);
+  e.taps.swap(m->taps);
+  e.exec = m->graph_exec;
+  e.uses = m->plan_uses;
+  e.used = ++m->clock;
+  m->graph_exec = nullptr;
+  m->plan_n = m->plan_t = -1;
+  m->cache.push_back(std::move(e));
+}
+
 static int build_plan(vox_model* m, const float* x, int n, int t, float* out) {
   auto run = [&](bool dry) -> int {
     Builder B{m, dry, &m->plan};
@@ -1614,13 +1691,11 @@ static int build_plan(vox_model* m, const float* x, int n, int t, float* out) {
     return fail(VOX_EINVAL, "unknown family");
   };
   // the previous plan's last launch may still be running on a caller's stream:
-  // its graph exec (and the kernel arguments HIP keeps with it) and the slots
-  // it reads and writes must outlive it
-  if (m->done) HIPCHK(hipEventSynchronize(m->done));
-  if (m->graph_exec) {
-    (void)hipGraphExecDestroy(m->graph_exec);
-    m->graph_exec = nullptr;
-  }
+  // a graph exec (and the kernel arguments HIP keeps with it) and the slots
+  // it reads and writes must outlive it.  The current plan moves to the cache
+  // (the least recently used entry is destroyed when it is full); building the
+  // new plan touches host memory only, so no wait unless something is freed
+  stash_current(m);
   int rc = run(true);
   if (rc) return rc;
   // slack: kernels with a K padded to 32 (gemm1x1_ws prologue / taps) read up to
@@ -1633,6 +1708,10 @@ static int build_plan(vox_model* m, const float* x, int n, int t, float* out) {
   for (int s = 0; s < S_NSLOTS; ++s) {
     const size_t want = m->slot_need[s] + 4096;
     if (want <= m->slots[s].bytes) continue;
+    if (!grew) {   // every cached plan points into the slots; the last launch may use them
+      if (m->done) HIPCHK(hipEventSynchronize(m->done));
+      drop_cache(m);
+    }
     HIPCHK(m->slots[s].ensure(want));
     HIPCHK(hipMemsetAsync(m->slots[s].p, 0, m->slots[s].bytes, m->stream));
     grew = true;
@@ -1644,6 +1723,8 @@ static int build_plan(vox_model* m, const float* x, int n, int t, float* out) {
   m->plan_t = t;
   m->plan_x = x;
   m->plan_out = out;
+  m->plan_uses = 0;
+  ++m->plans_built;
   return VOX_OK;
 }
 
@@ -1707,6 +1788,25 @@ static int check_shape(vox_model* m, int n, int t, int f) {
 
 static int ensure_plan(vox_model* m, const float* d_x, int n, int t, float* d_out) {
   if (m->plan_n == n && m->plan_t == t && m->plan_x == d_x && m->plan_out == d_out) return VOX_OK;
+  for (PlanEntry& e : m->cache) {
+    if (e.n != n || e.t != t || e.x != d_x || e.out != d_out) continue;
+    // swap the resident plan in; the current one takes its cache entry
+    std::swap(e.n, m->plan_n);
+    std::swap(e.t, m->plan_t);
+    std::swap(e.x, m->plan_x);
+    std::swap(e.out, m->plan_out);
+    e.plan.swap(m->plan);
+    e.taps.swap(m->taps);
+    std::swap(e.exec, m->graph_exec);
+    std::swap(e.uses, m->plan_uses);
+    e.used = ++m->clock;
+    if (e.n < 0) {   // there was no current plan
+      if (e.exec) (void)hipGraphExecDestroy(e.exec);
+      m->cache.erase(m->cache.begin() + (&e - m->cache.data()));
+    }
+    ++m->plan_hits;
+    return VOX_OK;
+  }
   return build_plan(m, d_x, n, t, d_out);
 }
 
@@ -1739,6 +1839,8 @@ extern "C" int vox_load_blob(const void* blob, size_t nbytes, int device, int pr
   if (!spec.get("bn_eps_4d").empty()) m->eps4 = std::strtof(spec.get("bn_eps_4d").c_str(), nullptr);
   if (!spec.get("bn_eps_2d").empty()) m->eps2 = std::strtof(spec.get("bn_eps_2d").c_str(), nullptr);
   if (const char* e = std::getenv("VOXEMB_NO_GRAPH")) m->use_graph = std::atoi(e) == 0;
+  if (const char* e = std::getenv("VOXEMB_PLAN_CACHE")) m->cache_max = std::max(0, std::atoi(e));
+  if (const char* e = std::getenv("VOXEMB_GRAPH_AFTER")) m->graph_after = std::max(0, std::atoi(e));
   for (const PlanEnv& pe : kPlanEnv)
     if (const char* e = std::getenv(pe.name)) m.get()->*pe.field = std::atoi(e);
 #ifndef VOX_DIAG
@@ -1773,8 +1875,20 @@ extern "C" void vox_free(vox_model* m) {
   }
   (void)hipDeviceSynchronize();   // replays launched on callers' streams
   if (m->graph_exec) (void)hipGraphExecDestroy(m->graph_exec);
+  for (PlanEntry& e : m->cache)
+    if (e.exec) (void)hipGraphExecDestroy(e.exec);
   if (m->done) (void)hipEventDestroy(m->done);
   delete m;
+}
+
+extern "C" int vox_plan_stats(const vox_model* m, int64_t* built, int64_t* hits, int64_t* dropped,
+                              int* resident) {
+  if (!m) return fail(VOX_EINVAL, "null handle");
+  if (built) *built = m->plans_built;
+  if (hits) *hits = m->plan_hits;
+  if (dropped) *dropped = m->plans_dropped;
+  if (resident) *resident = (int)m->cache.size() + (m->plan_n >= 0 ? 1 : 0);
+  return VOX_OK;
 }
 
 extern "C" int vox_dim(const vox_model* m) { return m ? m->out_dim : VOX_EINVAL; }
@@ -1792,7 +1906,7 @@ extern "C" int vox_embed_device(vox_model* m, const float* d_x, int n, int t, in
   HIPCHK(hipSetDevice(m->device));
   if ((rc = ensure_plan(m, d_x, n, t, d_out))) return rc;
   hipStream_t s = stream ? (hipStream_t)stream : m->stream;
-  if (m->use_graph && !m->graph_exec) {
+  if (m->use_graph && !m->graph_exec && m->plan_uses >= m->graph_after) {
     // capture on the handle's own stream (the caller's may be the legacy null
     // stream, which cannot be captured); the exec then launches on any stream
     hipGraph_t g = nullptr;
@@ -1819,6 +1933,7 @@ extern "C" int vox_embed_device(vox_model* m, const float* d_x, int n, int t, in
     for (const Op& op : m->plan) HIPCHK(run_op(m, op, s));
   }
   HIPCHK(hipEventRecord(m->done, s));
+  ++m->plan_uses;
   return VOX_OK;
 }
 

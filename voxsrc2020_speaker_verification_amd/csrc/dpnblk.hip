@@ -873,7 +873,7 @@ int dpn_block_ok(const DpnBlockParams& p) {
          p.cin % 8 == 0 && p.cin <= p.ldx && p.kp3 == DB_R &&
          (p.from_a ? p.cin == DB_R : (p.kp1 >= p.cin && p.kp1 <= 128)) &&
          p.ldx % 8 == 0 && p.ldy % 8 == 0 && p.ldr % 8 == 0 && p.bw <= p.ldr &&
-         p.bw % 8 == 0 && p.bw <= p.cout && p.cout <= 96 && p.cout % 8 == 0 && p.H > 0 &&
+         p.bw <= 8 * (DB_RXS - 2) && p.bw % 8 == 0 && p.bw <= p.cout && p.cout <= 96 && p.cout % 8 == 0 && p.H > 0 &&
          p.N > 0 && p.seg > 0 && p.nseg > 0 && (long)p.seg * p.nseg >= p.H;
 }
 

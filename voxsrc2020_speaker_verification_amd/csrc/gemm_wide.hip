@@ -776,7 +776,7 @@ hipError_t launch_gemm_wide(const ConvParams& p0, int num_cu, int variant, hipSt
   const int M = p.N * p.Ho * p.Wo;
   const int T = ((M + GW_BM - 1) / GW_BM) * (p.coutp / bn);
   int G = num_cu < T ? num_cu : T;
-  G = G / 8 * 8;
+  G = G >= 8 ? G / 8 * 8 : G;   // small launches (any_m) keep their few tiles
   const size_t lds = GW_NST * GW_SLOT + 8 * (size_t)p.coutp + (p.in_mean ? 8 * (size_t)p.kp : 0);
   // (the 320-wide tile holds 80 accumulators per compute wave at 128 pixels)
   const int bm = bn == 320 ? 128 : ws_bm(M, p.coutp / bn, bn, num_cu);

@@ -1507,12 +1507,16 @@ __global__ __launch_bounds__(64 * TS, PRO ? 4 : 1) void stats_pool_k(const T* __
 // Sequential summation over h (a fixed order per column, batch-independent).
 template <int VN> struct PoolRaw { typedef unsigned t __attribute__((ext_vector_type(VN / 2))); };
 template <> struct PoolRaw<2> { typedef unsigned t; };
-template <int HM, int VN>
+// PRO: DPN68's concat_bn_relu applied to each row as it lands (bnrelu_k's
+// rounding, as stats_pool_k<..., true>), the rows kept packed after it.
+template <int HM, int VN, bool PRO = false>
 __global__ __launch_bounds__(256) void stats_pool_col(const bf16_t* __restrict__ x, int N, int H,
                                                       int W, int C,
                                                       const float* __restrict__ mean,
                                                       const float* __restrict__ inv,
-                                                      float* __restrict__ out) {
+                                                      float* __restrict__ out,
+                                                      const float* __restrict__ in_mean = nullptr,
+                                                      const float* __restrict__ in_inv = nullptr) {
   typedef __bf16 bfv __attribute__((ext_vector_type(VN)));
   typedef typename PoolRaw<VN>::t uv;
   typedef float fv __attribute__((ext_vector_type(VN)));
@@ -1528,6 +1532,22 @@ __global__ __launch_bounds__(256) void stats_pool_col(const bf16_t* __restrict__
 #pragma unroll
   for (int h = 0; h < HM; ++h)
     if (h < H) v[h] = *reinterpret_cast<const uv*>(base + (size_t)h * rowstride);
+  if constexpr (PRO) {
+    float pm[VN], pi[VN];
+#pragma unroll
+    for (int e = 0; e < VN; ++e) {
+      pm[e] = in_mean[ch * VN + e];
+      pi[e] = in_inv[ch * VN + e];
+    }
+#pragma unroll
+    for (int h = 0; h < HM; ++h)
+      if (h < H) {
+        bfv b = __builtin_bit_cast(bfv, v[h]);
+#pragma unroll
+        for (int e = 0; e < VN; ++e) b[e] = (bf16_t)fmaxf(((float)b[e] - pm[e]) * pi[e], 0.f);
+        v[h] = __builtin_bit_cast(uv, b);
+      }
+  }
   float s[VN], q[VN];
 #pragma unroll
   for (int e = 0; e < VN; ++e) s[e] = q[e] = 0.f;
@@ -1579,18 +1599,29 @@ static hipError_t stats_pool_ts(const T* x, int N, int H, int W, int C, const fl
                                 const float* in_inv, hipStream_t s) {
   const int64_t cols = (int64_t)N * W * (C / VN);
   if constexpr (sizeof(T) == 2 && VN == 8) {
-    if (H <= 32 && !in_mean) {
+    if (H <= 32) {
       const unsigned b = (unsigned)((cols * 2 + 255) / 256);
       // 2 channels (4 B) per thread: at the headline (H = 25, T = 200) 2.5 grid
       // rounds of 8 waves per SIMD instead of 1.25 rounds at 7 (68 VGPRs with 4
       // channels), 35 -> 31 us in place; <16, 4> had compiled to 248 VGPRs.
-      // Same per-element summation order as 4 channels per thread: same bits
+      // Same per-element summation order as 4 channels per thread: same bits.
+      // With DPN68's prologue (in_mean) the PRO form, so the fused pool sums the
+      // same bnrelu_k-rounded rows in the same order as bnrelu + stats_pool_col
+      if (in_mean) {
+        if (H <= 16)
+          hipLaunchKernelGGL((stats_pool_col<16, 2, true>), dim3(2 * b), dim3(256), 0, s, x, N, H, W, C, mean, inv, out, in_mean, in_inv);
+        else if (H <= 25)
+          hipLaunchKernelGGL((stats_pool_col<25, 2, true>), dim3(2 * b), dim3(256), 0, s, x, N, H, W, C, mean, inv, out, in_mean, in_inv);
+        else
+          hipLaunchKernelGGL((stats_pool_col<32, 2, true>), dim3(2 * b), dim3(256), 0, s, x, N, H, W, C, mean, inv, out, in_mean, in_inv);
+        return hipGetLastError();
+      }
       if (H <= 16)
-        hipLaunchKernelGGL((stats_pool_col<16, 2>), dim3(2 * b), dim3(256), 0, s, x, N, H, W, C, mean, inv, out);
+        hipLaunchKernelGGL((stats_pool_col<16, 2>), dim3(2 * b), dim3(256), 0, s, x, N, H, W, C, mean, inv, out, nullptr, nullptr);
       else if (H <= 25)
-        hipLaunchKernelGGL((stats_pool_col<25, 2>), dim3(2 * b), dim3(256), 0, s, x, N, H, W, C, mean, inv, out);
+        hipLaunchKernelGGL((stats_pool_col<25, 2>), dim3(2 * b), dim3(256), 0, s, x, N, H, W, C, mean, inv, out, nullptr, nullptr);
       else
-        hipLaunchKernelGGL((stats_pool_col<32, 2>), dim3(2 * b), dim3(256), 0, s, x, N, H, W, C, mean, inv, out);
+        hipLaunchKernelGGL((stats_pool_col<32, 2>), dim3(2 * b), dim3(256), 0, s, x, N, H, W, C, mean, inv, out, nullptr, nullptr);
       return hipGetLastError();
     }
   }

@@ -72,6 +72,13 @@ class Extractor:
     def __exit__(self, *a):
         self.close()
 
+    def plan_stats(self):
+        """{built, hits, dropped, resident}: the native plan residency counters
+        (vox_plan_stats)."""
+        b, h, d, r = C.c_int64(), C.c_int64(), C.c_int64(), C.c_int()
+        check(lib().vox_plan_stats(self._h, C.byref(b), C.byref(h), C.byref(d), C.byref(r)))
+        return {"built": b.value, "hits": h.value, "dropped": d.value, "resident": r.value}
+
     # -- sess.run ---------------------------------------------------------
     def run(self, x):
         x = np.ascontiguousarray(x, dtype=np.float32)
