@@ -212,6 +212,20 @@ int vox_parse_mat_shape(const uint8_t* buf, size_t nbytes, int* rows, int* cols)
 int vox_read_mat_kaldi(const char* path, int64_t offset, float* out, int rows, int cols);
 int vox_parse_mat_kaldi(const uint8_t* buf, size_t nbytes, float* out, int rows, int cols,
                         size_t* consumed);
+/* Batched reader of the extraction path (the tf_extract.py get_batch process
+ * and its apply-cmvn-sliding rspec pipe, :63,:85-90) on `threads` host threads.
+ * vox_mat_shapes: rows/cols of n matrices at paths[i]:offsets[i], headers only.
+ * vox_read_chunks: one batch of n equal-length chunks -- item i is rows
+ * [r0[i], r0[i] + T[i]) and columns [c0[i], c0[i] + f) of the matrix at
+ * paths[i]:offsets[i] (an scp rxfile with its optional [range]; CM decoded in
+ * Kaldi C++'s arithmetic), sliding CMN over those T[i] rows when cmn_window > 0
+ * (window cmn_window, centered; bit-identical to vox_sliding_cmn of the whole
+ * utterance), then frames [start[i], start[i] + len) into out + i*len*f. */
+int vox_mat_shapes(const char* const* paths, const int64_t* offsets, int n, int* rows, int* cols,
+                   int threads);
+int vox_read_chunks(const char* const* paths, const int64_t* offsets, const int* r0, const int* T,
+                    const int* c0, const int* start, int n, int f, int len, int cmn_window,
+                    float* out, int threads);
 /* Serialise "key \0BFV \4<u32 dim><dim f32>" into buf; returns bytes written
  * (or needed, if cap is too small) and the offset of "\0B" via *data_offset. */
 int64_t vox_format_vec_flt(const char* key, const float* v, int dim, uint8_t* buf,

@@ -17,6 +17,7 @@
 #include "../../include/voxemb.h"
 
 int vox_set_error(int code, const char*) { return code; }   // api.cpp's, minus the message
+extern "C" const char* vox_last_error(void) { return ""; }
 
 static std::vector<uint8_t> slurp(const char* path) {
   std::ifstream f(path, std::ios::binary);
@@ -108,6 +109,50 @@ int main(int argc, char** argv) {
       std::vector<float> m((size_t)rows * cols + 1);
       (void)vox_read_mat(argv[a], off, m.data(), rows, cols);
       (void)vox_read_mat_kaldi(argv[a], off, m.data(), rows, cols);
+    }
+  }
+  // batched readers (vox_mat_shapes / vox_read_chunks, 3 host threads): every
+  // matrix each file holds, whole and as [range] chunks, against the
+  // single-matrix reader + whole-utterance CMN bit for bit; then forged ranges
+  for (int a = 1; a < argc; ++a) {
+    const std::vector<uint8_t> b = slurp(argv[a]);
+    std::vector<int64_t> offs;
+    for (int64_t off = 0; off < (int64_t)b.size(); ++off) {
+      int rows = 0, cols = 0;
+      if (b[off] == '\0' && vox_mat_shape(argv[a], off, &rows, &cols) == VOX_OK && rows > 0 &&
+          cols > 0 && (int64_t)rows * cols <= (int64_t)1 << 22 && (off == 0 || b[off - 1] == ' '))
+        offs.push_back(off);
+    }
+    const int n = (int)offs.size();
+    if (!n) continue;
+    std::vector<const char*> paths(n, argv[a]);
+    std::vector<int> rows(n), cols(n);
+    if (vox_mat_shapes(paths.data(), offs.data(), n, rows.data(), cols.data(), 3) != VOX_OK) return 5;
+    for (int i = 0; i < n; ++i) {
+      const int T = rows[i], F = cols[i];
+      std::vector<float> m((size_t)T * F), c((size_t)T * F);
+      if (vox_read_mat_kaldi(argv[a], offs[i], m.data(), T, F) != VOX_OK) return 5;
+      if (vox_sliding_cmn(m.data(), T, F, 300, 1, c.data()) != VOX_OK) return 5;
+      for (int len : {T, (T + 1) / 2, 1}) {
+        const int start = T - len, r0 = 0, c0 = 0;
+        std::vector<float> o((size_t)len * F);
+        for (int cmn = 0; cmn < 2; ++cmn) {
+          if (vox_read_chunks(&paths[i], &offs[i], &r0, &T, &c0, &start, 1, F, len, cmn ? 300 : 0,
+                              o.data(), 3) != VOX_OK)
+            return 5;
+          const float* ref = (cmn ? c.data() : m.data()) + (size_t)start * F;
+          if (std::memcmp(o.data(), ref, o.size() * 4) != 0) return 6;
+        }
+      }
+    }
+    // forged ranges / starts: rejected or in bounds, never a sanitizer report
+    for (int it = 0; it < 200; ++it) {
+      const int i = (int)(rng() % n);
+      const int r0 = (int)(rng() % (rows[i] + 2)) - 1, T = (int)(rng() % (rows[i] + 2));
+      const int c0 = (int)(rng() % 3) - 1, st = (int)(rng() % (rows[i] + 2)) - 1;
+      const int len = 1 + (int)(rng() % (rows[i] + 1));
+      std::vector<float> o((size_t)len * cols[i] + 1);
+      (void)vox_read_chunks(&paths[i], &offs[i], &r0, &T, &c0, &st, 1, cols[i], len, 300, o.data(), 2);
     }
   }
   // sliding CMN on edge shapes (T = 1, window > T, odd windows, centre off)

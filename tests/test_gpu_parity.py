@@ -806,3 +806,35 @@ def test_resident_plans_alternating_shapes(weights, monkeypatch):
         for s in shapes:
             assert np.array_equal(ex.run(xs[s]), ref[s])
         assert ex.plan_stats()["built"] == len(shapes) - 0 and ex.plan_stats()["resident"] == 1
+
+
+@pytest.mark.parametrize("lanes", [1, 3])
+def test_stream_lanes_equal_in_memory_path(weights, tmp_path, lanes):
+    """The streaming pipeline (stream.extract_entries: header planning, native
+    batched reader, `lanes` handles on their own streams) gives the same bits
+    as decoding the whole shard and running the chunk loop through one
+    handle's host API (the round-4 extract.py path), bf16 Res2Net, lengths
+    across the 1000-frame chunk boundary, batches of 3."""
+    from voxsrc2020_speaker_verification_amd import extract, kaldi, synth
+    from voxsrc2020_speaker_verification_amd.stream import extract_entries
+    spec, t, blob = weights("res2net50_w24_s4_c32", 80)
+    rng = np.random.default_rng(11)
+    lens = [30, 1030, 2500, 999, 1000, 1001, 25, 2000, 180, 180, 180, 180, 999, 260]
+    mats = [(f"u{i:02d}", (rng.standard_normal((T, 80)) * 2 + 1).astype(np.float32))
+            for i, T in enumerate(lens)]
+    scp = _write_fm_ark(str(tmp_path / "f.ark"), mats)
+    (tmp_path / "f.scp").write_text("".join(scp))
+    entries = kaldi.read_scp(str(tmp_path / "f.scp"))
+    exs = [_extractor(blob, "bf16") for _ in range(lanes)]
+    try:
+        keys, got = extract_entries(entries, exs, batch=3)
+        stats = [e.plan_stats() for e in exs]
+    finally:
+        for e in exs:
+            e.close()
+    with _extractor(blob, "bf16") as ex:
+        feats = list(kaldi.iter_features(str(tmp_path / "f.scp")))
+        ref = extract.embed_utterances(feats, ex.run, ex.dim, 3)
+    assert keys == [k for k, _ in mats]
+    assert np.array_equal(got, ref)
+    assert sum(s["built"] for s in stats) >= 1

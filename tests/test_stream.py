@@ -1,0 +1,119 @@
+"""The streaming extraction pipeline (stream.py) on the CPU: planning from the
+matrix headers, the native batched chunk reader and the per-utterance
+combination give exactly what the in-memory path gives (whole shard decoded
+with kaldi.iter_features, then extract.embed_utterances), for a deterministic
+row-wise stand-in of the network.  The GPU lanes are covered by
+tests/test_gpu_parity.py (test_extract_cli_end_to_end, test_stream_lanes_*)."""
+
+import os
+import struct
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _fm_ark(path, mats):
+    """Binary FM ark as kaldi_io.write_mat writes it; returns scp lines."""
+    lines = []
+    with open(path, "wb") as f:
+        for key, m in mats:
+            f.write(key.encode() + b" ")
+            off = f.tell()
+            f.write(b"\0BFM \x04" + struct.pack("<i", m.shape[0]) + b"\x04" +
+                    struct.pack("<i", m.shape[1]) + m.astype("<f4").tobytes())
+            lines.append(f"{key} {path}:{off}")
+    return lines
+
+
+def _embed(x):
+    """Row-wise, batch-independent stand-in for the network: [n, L, F] -> [n, 2F]."""
+    x64 = x.astype(np.float64)
+    return np.concatenate([x64.mean(1), np.abs(x64).max(1) * (x.shape[1] % 7 + 1)], 1).astype(np.float32)
+
+
+@pytest.fixture
+def shard(tmp_path):
+    rng = np.random.default_rng(7)
+    lens = [30, 1030, 2500, 999, 1000, 1001, 25, 2000, 1024, 1025, 180, 180, 999]
+    mats = [(f"u{i:03d}", (rng.standard_normal((T, 40)) * 3 + 2).astype(np.float32))
+            for i, T in enumerate(lens)]
+    lines = _fm_ark(str(tmp_path / "a.ark"), mats[:7]) + _fm_ark(str(tmp_path / "b.ark"), mats[7:])
+    # an rxfile [range] (rows 100..1299, columns 0..39) as Kaldi's scp allows
+    key, rx = lines[2].split()
+    lines.append(f"u_rng {rx}[100:1299,0:39]")
+    scp = tmp_path / "feats.scp"
+    scp.write_text("\n".join(lines) + "\n")
+    return str(scp)
+
+
+@pytest.mark.parametrize("batch", [1, 3, 64])
+def test_streamed_equals_in_memory(shard, batch):
+    from voxsrc2020_speaker_verification_amd import extract, kaldi
+    feats = list(kaldi.iter_features(shard))
+    ref = extract.embed_utterances(feats, _embed, 80, batch)
+    keys, got = extract.extract_scp(shard, _embed, 80, batch, threads=3)
+    assert keys == [k for k, _ in feats]
+    assert got.dtype == np.float32 and np.array_equal(got, ref)
+
+
+def test_reader_matches_whole_utterance_cmn(shard):
+    """vox_read_chunks == sliding CMN of the whole (ranged) utterance, sliced."""
+    from voxsrc2020_speaker_verification_amd import kaldi
+    from voxsrc2020_speaker_verification_amd.stream import ChunkTable, plan_batches
+    entries = kaldi.read_scp(shard)
+    feats = dict(kaldi.iter_features(shard))
+    table = ChunkTable(entries, threads=4)
+    assert list(table.T) == [feats[k].shape[0] for k in table.keys]
+    _, batches = plan_batches(table.T, 5)
+    for L, items in batches:
+        x = np.empty((len(items), L, 40), np.float32)
+        table.read(items, L, x)
+        for row, (u, ci, s) in zip(x, items):
+            assert np.array_equal(row, feats[table.keys[u]][s:s + L])
+
+
+def test_compressed_ark_reader():
+    """CM arks decode in Kaldi C++'s arithmetic through the batched reader."""
+    from voxsrc2020_speaker_verification_amd import kaldi
+    from voxsrc2020_speaker_verification_amd.stream import ChunkTable
+    ark = os.path.join(HERE, "golden", "cm_mats.ark")
+    entries, pos = [], 0
+    buf = open(ark, "rb").read()
+    while pos < len(buf):
+        sp = buf.index(b" ", pos)
+        key = buf[pos:sp].decode()
+        mat, used = kaldi.parse_mat(buf[sp + 1:], cm="kaldi")
+        entries.append((key, f"{ark}:{sp + 1}", mat))
+        pos = sp + 1 + used
+    assert len(entries) >= 2
+    for k, rx, mat in entries:     # (the golden matrices differ in width: one table each)
+        table = ChunkTable([(k, rx)], threads=2)
+        T = mat.shape[0]
+        x = np.empty((1, T, mat.shape[1]), np.float32)
+        table.read([(0, 0, 0)], T, x, cmn=False)
+        assert np.array_equal(x[0], mat), k
+
+
+def test_plan_batches_order_and_short_utterance():
+    from voxsrc2020_speaker_verification_amd.stream import plan_batches
+    plans, batches = plan_batches([30, 1030, 2500, 999], 2)
+    assert plans[2] == [(0, 1000), (1000, 1000), (2000, 500)]
+    sizes = [L * len(it) for L, it in batches]
+    assert sizes == sorted(sizes, reverse=True)
+    assert sorted((u, ci) for _, it in batches for u, ci, _ in it) == \
+        [(0, 0), (1, 0), (1, 1), (2, 0), (2, 1), (2, 2), (3, 0)]
+    with pytest.raises(ZeroDivisionError):
+        plan_batches([30, 24], 4, keys=["a", "short"])
+
+
+def test_reader_errors_are_reported(tmp_path):
+    from voxsrc2020_speaker_verification_amd import _native
+    from voxsrc2020_speaker_verification_amd.stream import ChunkTable
+    with pytest.raises(_native.VoxError):
+        ChunkTable([("x", str(tmp_path / "missing.ark") + ":0")])
+    lines = _fm_ark(str(tmp_path / "c.ark"), [("k", np.zeros((40, 8), np.float32))])
+    t = ChunkTable([lines[0].split()], threads=1)
+    with pytest.raises(_native.VoxError):
+        t.read([(0, 0, 30)], 20, np.empty(20 * 8, np.float32))   # chunk past the end

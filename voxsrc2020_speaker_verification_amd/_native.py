@@ -77,6 +77,10 @@ _SIGS = [
     ("vox_parse_mat", C.c_int, [C.c_char_p, C.c_size_t, _F, C.c_int, C.c_int,
                                 C.POINTER(C.c_size_t)]),
     ("vox_read_mat_kaldi", C.c_int, [C.c_char_p, C.c_int64, _F, C.c_int, C.c_int]),
+    ("vox_mat_shapes", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int]),
+    ("vox_read_chunks", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                  C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                                  C.c_int]),
     ("vox_parse_mat_kaldi", C.c_int, [C.c_char_p, C.c_size_t, _F, C.c_int, C.c_int,
                                       C.POINTER(C.c_size_t)]),
     ("vox_parse_mat_shape", C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(C.c_int),

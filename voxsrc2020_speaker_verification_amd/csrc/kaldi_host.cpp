@@ -13,9 +13,11 @@
 //   * FV record writer (kaldi_io.write_vec_flt, kaldi_io.py:304-334).
 // Compiled with -ffp-contract=off so no multiply-add is fused.
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/voxemb.h"
@@ -23,13 +25,15 @@
 int vox_set_error(int code, const char* msg);  // api.cpp (shared thread-local message)
 static int kfail(int code, const char* msg) { return vox_set_error(code, msg); }
 
-extern "C" int vox_sliding_cmn(const float* in, int T, int F, int cmn_window, int center,
-                               float* out) {
-  if (!in || !out || T <= 0 || F <= 0 || cmn_window <= 0) return kfail(VOX_EINVAL, "bad cmn args");
+// The recursion over t in [0, t1) (the running sums always start at t = 0, so
+// every output row has the same bits as the whole-utterance pass); rows
+// t >= t0 are written to out[(t - t0) * F].
+static void sliding_cmn_rows(const float* in, int T, int F, int cmn_window, int center, int t0,
+                             int t1, float* out) {
   const int min_window = 100;  // Kaldi default (only used when center == false)
   std::vector<double> sum(F, 0.0);
   int last_start = -1, last_end = -1;
-  for (int t = 0; t < T; ++t) {
+  for (int t = 0; t < t1; ++t) {
     int ws, we;
     if (center) {
       ws = t - cmn_window / 2;
@@ -61,9 +65,16 @@ extern "C" int vox_sliding_cmn(const float* in, int T, int F, int cmn_window, in
     last_start = ws;
     last_end = we;
     const double alpha = -1.0 / n;
+    if (t < t0) continue;
     for (int f = 0; f < F; ++f)
-      out[(size_t)t * F + f] = (float)((double)in[(size_t)t * F + f] + alpha * sum[f]);
+      out[(size_t)(t - t0) * F + f] = (float)((double)in[(size_t)t * F + f] + alpha * sum[f]);
   }
+}
+
+extern "C" int vox_sliding_cmn(const float* in, int T, int F, int cmn_window, int center,
+                               float* out) {
+  if (!in || !out || T <= 0 || F <= 0 || cmn_window <= 0) return kfail(VOX_EINVAL, "bad cmn args");
+  sliding_cmn_rows(in, T, F, cmn_window, center, 0, T, out);
   return VOX_OK;
 }
 
@@ -318,4 +329,104 @@ extern "C" int64_t vox_format_vec_flt(const char* key, const float* v, int dim, 
   q += 4;
   std::memcpy(q, v, (size_t)dim * 4);
   return (int64_t)need;
+}
+
+// ------------------------------------------------------ batched chunk reader
+// The reader side of tf_extract.py (get_batch in its own process feeding a
+// Queue(32), :85-90; features through the apply-cmvn-sliding pipe, :63),
+// for a whole batch of equal-length chunks at once on `threads` workers.
+namespace {
+struct FirstError {
+  std::atomic<int> code{0};
+  std::string msg;
+  std::atomic_flag taken = ATOMIC_FLAG_INIT;
+  void set(int c, const char* m) {
+    if (!taken.test_and_set()) {
+      msg = m;
+      code.store(c);
+    }
+  }
+};
+
+template <typename F>
+void parallel_for(int n, int threads, F&& body) {
+  threads = std::max(1, std::min(threads, n));
+  std::atomic<int> next{0};
+  auto work = [&]() {
+    for (int i; (i = next.fetch_add(1)) < n;) body(i);
+  };
+  std::vector<std::thread> pool;
+  for (int k = 1; k < threads; ++k) pool.emplace_back(work);
+  work();
+  for (auto& t : pool) t.join();
+}
+
+// header only (no payload read): rows / cols of the matrix at path:offset
+int read_shape_at(const char* path, int64_t offset, int* rows, int* cols) {
+  FILE* f = std::fopen(path, "rb");
+  if (!f) return kfail(VOX_EIO, "cannot open matrix file");
+  uint8_t head[64];
+  size_t got = 0;
+  if (offset >= 0 && std::fseek(f, (long)offset, SEEK_SET) == 0) got = std::fread(head, 1, sizeof(head), f);
+  std::fclose(f);
+  if (got == 0) return kfail(VOX_EIO, "offset beyond end of file");
+  Reader r{head, got};
+  int kind;
+  return parse_header(r, rows, cols, &kind);
+}
+}  // namespace
+
+extern "C" int vox_mat_shapes(const char* const* paths, const int64_t* offsets, int n, int* rows,
+                              int* cols, int threads) {
+  if (n < 0 || (n > 0 && (!paths || !offsets || !rows || !cols))) return kfail(VOX_EINVAL, "null argument");
+  FirstError err;
+  parallel_for(n, threads, [&](int i) {
+    if (err.code.load()) return;
+    const int rc = paths[i] ? read_shape_at(paths[i], offsets[i], &rows[i], &cols[i])
+                            : kfail(VOX_EINVAL, "null path");
+    if (rc) err.set(rc, (std::string(paths[i] ? paths[i] : "?") + ": " + vox_last_error()).c_str());
+  });
+  if (err.code.load()) return kfail(err.code.load(), err.msg.c_str());
+  return VOX_OK;
+}
+
+extern "C" int vox_read_chunks(const char* const* paths, const int64_t* offsets, const int* r0,
+                               const int* T, const int* c0, const int* start, int n, int f,
+                               int len, int cmn_window, float* out, int threads) {
+  if (n < 0 || f <= 0 || len <= 0 || (n > 0 && (!paths || !offsets || !r0 || !T || !c0 || !start || !out)))
+    return kfail(VOX_EINVAL, "bad arguments");
+  FirstError err;
+  parallel_for(n, threads, [&](int i) {
+    if (err.code.load()) return;
+    auto bad = [&](int rc) {
+      err.set(rc, (std::string(paths[i] ? paths[i] : "?") + ": " + vox_last_error()).c_str());
+    };
+    if (!paths[i] || T[i] <= 0 || r0[i] < 0 || c0[i] < 0 || start[i] < 0 || start[i] + len > T[i])
+      return bad(kfail(VOX_EINVAL, "chunk outside its utterance"));
+    thread_local std::vector<uint8_t> buf;
+    thread_local std::vector<float> mat, utt;
+    int rc = read_file_at(paths[i], offsets[i], buf);
+    if (rc) return bad(rc);
+    Reader r{buf.data(), buf.size()};
+    int rows, cols, kind;
+    if ((rc = parse_header(r, &rows, &cols, &kind))) return bad(rc);
+    if (r0[i] + T[i] > rows || c0[i] + f > cols) return bad(kfail(VOX_EINVAL, "range outside the matrix"));
+    mat.resize((size_t)rows * cols);
+    // Kaldi's CompressedMatrix arithmetic: what apply-cmvn-sliding decodes (tf_extract.py:63)
+    if ((rc = parse_payload(r, kind, rows, cols, mat.data(), 1))) return bad(rc);
+    const float* u = mat.data();
+    if (r0[i] != 0 || T[i] != rows || c0[i] != 0 || f != cols) {   // the rxfile's [range]
+      utt.resize((size_t)T[i] * f);
+      for (int t = 0; t < T[i]; ++t)
+        std::memcpy(&utt[(size_t)t * f], &mat[(size_t)(r0[i] + t) * cols + c0[i]], (size_t)f * 4);
+      u = utt.data();
+    }
+    float* o = out + (size_t)i * len * f;
+    if (cmn_window > 0)
+      sliding_cmn_rows(u, T[i], f, cmn_window, 1, start[i], start[i] + len, o);
+    else
+      std::memcpy(o, u + (size_t)start[i] * f, (size_t)len * f * 4);
+  });
+  if (err.code.load()) return kfail(err.code.load(), err.msg.c_str());
+  return VOX_OK;
 }

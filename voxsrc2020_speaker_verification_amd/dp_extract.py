@@ -112,7 +112,7 @@ def completed_shard(wspec, rank, keys, dim, tag=None):
 
 def run(rank, world, scp_items, embed_fn, dim, wspec, shard_file=None, batch=64,
         device=None, write_per_rank=True, cohort_spk2utt=None, resume=False, shard_keys=None,
-        tag=None):
+        tag=None, extract_shard=None):
     """The per-rank body (also used by the gloo tests with a fake embedder).
     scp_items: full list of (key, feat) is NOT required -- each rank only
     decodes its own shard: `scp_items` is a callable(rank, world) -> list of
@@ -121,7 +121,9 @@ def run(rank, world, scp_items, embed_fn, dim, wspec, shard_file=None, batch=64,
     reuses them -- the reference's per-shard processes are restartable one by
     one in the same way (eval_inference_model.sh:29-36).  tag: the run tag
     (run_tag) written beside each per-rank pair and required to match on
-    resume."""
+    resume.  extract_shard: callable(rank, world) -> (keys, [n, dim]
+    embeddings) that replaces scp_items + embed_fn (the CLI's streaming GPU
+    pipeline, stream.extract_entries: the shard is never decoded whole)."""
     from .extract import embed_utterances, write_vectors
     err = None
     try:
@@ -129,7 +131,9 @@ def run(rank, world, scp_items, embed_fn, dim, wspec, shard_file=None, batch=64,
         if resume and wspec and shard_keys is not None:
             keys = list(shard_keys(rank, world))
             emb = completed_shard(wspec, rank, keys, dim, tag)
-        if emb is None:
+        if emb is None and extract_shard is not None:
+            keys, emb = extract_shard(rank, world)
+        elif emb is None:
             feats = scp_items(rank, world)
             emb = (embed_utterances(feats, embed_fn, dim, batch) if feats
                    else np.zeros((0, dim), np.float32))
@@ -175,6 +179,9 @@ def main(argv=None):
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--cohort-spk2utt", default=None)
+    ap.add_argument("--lanes", type=int, default=4,
+                    help="concurrent extraction handles / streams per GPU")
+    ap.add_argument("--reader-threads", type=int, default=None)
     ap.add_argument("--resume", action="store_true",
                     help="reuse per-rank xvector.<i>.ark/.scp that already hold the rank's shard")
     a = ap.parse_args(argv)
@@ -189,34 +196,31 @@ def main(argv=None):
     torch.cuda.set_device(local)
     dist.init_process_group("nccl", rank=rank, world_size=world,
                             device_id=torch.device("cuda", local))
-    from .extractor import Extractor
-    from .kaldi import iter_features
+    from .extract import open_lanes
+    from .kaldi import read_scp
     from .partition import shard
+    from .stream import extract_entries
 
-    def items(r, w):
+    def entries(r, w):
         if a.pre_split:
-            return list(iter_features(f"{a.rspec}.{r + 1}.scp"))
-        from .kaldi import parse_rxfile, read_mat, read_scp, sliding_cmn
-        lines = shard(read_scp(a.rspec + ".scp"), r, w)
-        out = []
-        for key, rx in lines:
-            path, off, rng = parse_rxfile(rx)
-            m = read_mat(path, off, cm="kaldi")   # Kaldi decodes CM in the reference pipe
-            if rng is not None:
-                m = np.ascontiguousarray(m[rng])
-            out.append((key, sliding_cmn(m)))
-        return out
+            return read_scp(f"{a.rspec}.{r + 1}.scp")
+        return shard(read_scp(a.rspec + ".scp"), r, w)
 
     def keys(r, w):
-        from .kaldi import read_scp
-        if a.pre_split:
-            return [k for k, _ in read_scp(f"{a.rspec}.{r + 1}.scp")]
-        return [k for k, _ in shard(read_scp(a.rspec + ".scp"), r, w)]
+        return [k for k, _ in entries(r, w)]
 
-    with Extractor(a.pb_file, device=local, precision=a.precision) as ex:
-        run(rank, world, items, ex.run, ex.dim, a.wspec, batch=a.batch,
+    lanes = open_lanes(a.pb_file, local, a.precision, a.lanes)
+    try:
+        # the rank's shard streamed through its lanes (stream.py): planned from
+        # the matrix headers, decoded one batch of chunks at a time
+        run(rank, world, None, None, lanes[0].dim, a.wspec, batch=a.batch,
             device=torch.device("cuda", local), cohort_spk2utt=a.cohort_spk2utt,
-            resume=a.resume, shard_keys=keys, tag=run_tag(a.pb_file, a.precision))
+            resume=a.resume, shard_keys=keys, tag=run_tag(a.pb_file, a.precision),
+            extract_shard=lambda r, w: extract_entries(entries(r, w), lanes, a.batch,
+                                                       threads=a.reader_threads))
+    finally:
+        for ex in lanes:
+            ex.close()
     dist.barrier()
     dist.destroy_process_group()
     return 0

@@ -6,7 +6,10 @@ Reference: tensorflow/tf_extract.py:45-113.  Same flags (--pb-file,
 all result-preserving:
   * chunks of equal length are batched together (the reference runs batch 1,
     :27); embeddings are batch-independent (bitwise, tests/test_gpu_parity.py);
-  * no reader process / pickle queue: features are decoded natively;
+  * no reader process / pickle queue: the shard is planned from the matrix
+    headers, then each batch of chunks is decoded, CMN'd and sliced natively
+    into a bounded ring of pinned buffers while earlier batches run on
+    `--lanes` concurrent streams (stream.py);
   * --pb-file takes a VOXEMB01 weight blob (see weights.py / INTEGRATION.md);
   * an utterance shorter than 25 frames raises ZeroDivisionError, as the
     reference does at :111, before anything is written for later utterances.
@@ -58,11 +61,21 @@ def embed_utterances(feats, embed_batch, dim, batch=64, stack=np.stack):
     return out
 
 
-def extract_scp(scp_path, embed_batch, dim, batch=64, cmn=True):
-    """(keys, embeddings) for every utterance of an scp, in scp order."""
-    from .kaldi import iter_features
-    feats = list(iter_features(scp_path, cmn=cmn))
-    return [k for k, _ in feats], embed_utterances(feats, embed_batch, dim, batch)
+def extract_scp(scp_path, embed_batch, dim, batch=64, cmn=True, threads=None):
+    """(keys, embeddings) for every utterance of an scp, in scp order, through
+    a synchronous embed function (host numpy in and out), streamed: headers
+    first, then one batch of chunks at a time (stream.py)."""
+    from .kaldi import read_scp
+    from .stream import ChunkTable, SyncRunner, extract_stream
+    table = ChunkTable(read_scp(scp_path), threads)
+    keys, emb = extract_stream(table, lambda b: SyncRunner(table, embed_batch, cmn), batch)
+    return keys, (emb if emb is not None else np.zeros((0, dim), np.float32))
+
+
+def open_lanes(pb_file, device, precision, lanes):
+    """`lanes` extraction handles of one model on one device (stream.LanePool)."""
+    from .extractor import Extractor
+    return [Extractor(pb_file, device=device, precision=precision) for _ in range(max(1, lanes))]
 
 
 def write_vectors(base, keys, emb, atomic=False):
@@ -84,13 +97,25 @@ def main(argv=None):
     ap.add_argument("--device", type=int, default=0)
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--no-cmn", action="store_true", help="features are already CMN'd")
+    ap.add_argument("--lanes", type=int, default=4,
+                    help="concurrent extraction handles / streams on the device")
+    ap.add_argument("--reader-threads", type=int, default=None,
+                    help="host threads decoding + CMN'ing features (default: usable CPUs, <= 16)")
     a = ap.parse_args(argv)
-    from .extractor import Extractor
-    with Extractor(a.pb_file, device=a.device, precision=a.precision) as ex:
-        if ex.expand_dim != a.expand_dim:
+    import torch
+    from .kaldi import read_scp
+    from .stream import extract_entries
+    torch.cuda.set_device(a.device)
+    lanes = open_lanes(a.pb_file, a.device, a.precision, a.lanes)
+    try:
+        if lanes[0].expand_dim != a.expand_dim:
             print(f"warning: --expand-dim {a.expand_dim} but the model layout is "
-                  f"{ex.expand_dim}; using the model's", file=sys.stderr)
-        keys, emb = extract_scp(a.rspec + ".scp", ex.run, ex.dim, a.batch, cmn=not a.no_cmn)
+                  f"{lanes[0].expand_dim}; using the model's", file=sys.stderr)
+        keys, emb = extract_entries(read_scp(a.rspec + ".scp"), lanes, a.batch,
+                                    cmn=not a.no_cmn, threads=a.reader_threads)
+    finally:
+        for ex in lanes:
+            ex.close()
     write_vectors(a.wspec, keys, emb)
     return 0
 
