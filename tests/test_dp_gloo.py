@@ -34,21 +34,30 @@ def _items(n_utts):
     return feats, items
 
 
-def _worker(rank, world, port, outdir, n_utts):
+def _worker(rank, world, port, outdir, n_utts, streamed=False):
     import torch.distributed as dist
     from voxsrc2020_speaker_verification_amd import dp_extract
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
                             world_size=world)
     _, items = _items(n_utts)
     spk2utt = os.path.join(outdir, "spk2utt")
+    shard_fn = None
+    if streamed:   # the CLI's form: the rank's scp lines streamed (stream.py), never decoded whole
+        from voxsrc2020_speaker_verification_amd import kaldi, stream
+        from voxsrc2020_speaker_verification_amd.partition import shard
+
+        def shard_fn(r, w):
+            table = stream.ChunkTable(shard(kaldi.read_scp(os.path.join(outdir, "feats.scp")), r, w), 2)
+            return stream.extract_stream(
+                table, lambda b: stream.SyncRunner(table, _fake_embed, cmn=False), 3)
     dp_extract.run(rank, world, items, _fake_embed, 8, os.path.join(outdir, "xvector"),
-                   batch=3, cohort_spk2utt=spk2utt)
+                   batch=3, cohort_spk2utt=spk2utt, extract_shard=shard_fn)
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n_utts", [(2, 11), (3, 7)])
-def test_dp_extract_gloo(tmp_path, world, n_utts):
+@pytest.mark.parametrize("world,n_utts,streamed", [(2, 11, False), (3, 7, False), (2, 11, True)])
+def test_dp_extract_gloo(tmp_path, world, n_utts, streamed):
     import torch.multiprocessing as mp
     from voxsrc2020_speaker_verification_amd import kaldi
     from voxsrc2020_speaker_verification_amd.extract import embed_utterances
@@ -56,7 +65,14 @@ def test_dp_extract_gloo(tmp_path, world, n_utts):
     with open(tmp_path / "spk2utt", "w") as f:
         for s in range(3):
             f.write(f"spk{s} " + " ".join(k for k, _ in feats if k.startswith(f"spk{s}-")) + "\n")
-    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), n_utts), nprocs=world, join=True)
+    if streamed:
+        with open(tmp_path / "feats.ark", "wb") as fa, open(tmp_path / "feats.scp", "w") as fs:
+            for k, m in feats:
+                rec, off = kaldi.format_mat_flt(k, m)
+                fs.write(f"{k} {tmp_path / 'feats.ark'}:{fa.tell() + off}\n")
+                fa.write(rec)
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), n_utts, streamed), nprocs=world,
+             join=True)
     # merged ark is byte-identical to the concatenation of the per-rank arks
     cat = b"".join(open(tmp_path / f"xvector.{r + 1}.ark", "rb").read() for r in range(world))
     assert open(tmp_path / "xvector.ark", "rb").read() == cat

@@ -131,13 +131,14 @@ def run(rank, world, scp_items, embed_fn, dim, wspec, shard_file=None, batch=64,
         if resume and wspec and shard_keys is not None:
             keys = list(shard_keys(rank, world))
             emb = completed_shard(wspec, rank, keys, dim, tag)
-        if emb is None and extract_shard is not None:
-            keys, emb = extract_shard(rank, world)
-        elif emb is None:
-            feats = scp_items(rank, world)
-            emb = (embed_utterances(feats, embed_fn, dim, batch) if feats
-                   else np.zeros((0, dim), np.float32))
-            keys = [k for k, _ in feats]
+        if emb is None:
+            if extract_shard is not None:
+                keys, emb = extract_shard(rank, world)
+            else:
+                feats = scp_items(rank, world)
+                emb = (embed_utterances(feats, embed_fn, dim, batch) if feats
+                       else np.zeros((0, dim), np.float32))
+                keys = [k for k, _ in feats]
             if write_per_rank and wspec:
                 # xvector.<i>.ark as the reference; atomic for --resume
                 base = f"{wspec}.{rank + 1}"
