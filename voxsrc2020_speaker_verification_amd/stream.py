@@ -11,13 +11,14 @@ into a Queue(32), and the session runs each <= 1000-frame chunk on its own
      together bit for bit (embeddings are batch-independent), and the shard is
      one planning window, so real length distributions still give full batches;
   2. reading: each batch's chunks decoded, CMN'd and sliced straight into a
-     pinned host buffer by the native reader (`vox_read_chunks`, host threads),
-     one batch ahead of the GPU, into a bounded ring of buffers;
+     pinned host buffer by the native reader (`vox_read_chunks`, host threads)
+     while the lane's previous batch runs on the GPU;
   3. compute: the batches go round-robin to `lanes` extraction handles, each
-     with its own stream, device buffers and resident plans; the H2D copy, the
-     forward and the D2H copy of one batch are queued on its lane's stream.
+     driven by its own host thread with its own stream, device buffers and
+     resident plans; the H2D copy, the forward and the D2H copy of one batch
+     are queued on its lane's stream.
 
-Host memory is the ring (a few batches of features) plus one embedding per
+Host memory is two batches of features per lane plus one embedding per
 utterance; nothing grows with the features of the shard.  The per-utterance
 combination (length-weighted mean, :108-111) is the float32 arithmetic of
 `extract.embed_utterances`, so the arks are byte-identical to it.
@@ -25,10 +26,8 @@ combination (length-weighted mean, :108-111) is the float32 arithmetic of
 
 from __future__ import annotations
 
-import collections
 import ctypes as C
 import os
-from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
@@ -96,7 +95,7 @@ class ChunkTable:
     def __len__(self):
         return len(self.keys)
 
-    def read(self, items, L, out, cmn=True):
+    def read(self, items, L, out, cmn=True, threads=None):
         """Chunks [(u, ci, start)] of length L -> out ([>= n*L*F] float32, numpy
         array or torch tensor in host memory)."""
         n = len(items)
@@ -110,7 +109,8 @@ class ChunkTable:
         ptr = out.data_ptr() if hasattr(out, "data_ptr") else out.ctypes.data
         check(lib().vox_read_chunks(paths, offs.ctypes.data, r0.ctypes.data, T.ctypes.data,
                                     c0.ctypes.data, st.ctypes.data, n, self.feat_dim, int(L),
-                                    CMN_WINDOW if cmn else 0, C.c_void_p(ptr), self.threads))
+                                    CMN_WINDOW if cmn else 0, C.c_void_p(ptr),
+                                    threads or self.threads))
 
 
 def plan_batches(lengths, batch, keys=None):
@@ -179,87 +179,100 @@ class SyncRunner:
 
 
 class LanePool:
-    """`lanes` extraction handles on one device, each with its own stream,
-    input / output device buffers sized for the largest batch, and resident
-    plans; a ring of pinned host buffers filled by the native reader one or
-    more batches ahead."""
+    """`lanes` extraction handles on one device, each driven by its own host
+    thread: lane k takes batches k, k + K, k + 2K, ...; for each it reads the
+    chunks into one of its two pinned buffers with the native reader (the
+    GIL is released in every native call, so the lanes' reading, planning and
+    launching run in parallel), queues H2D + forward + D2H on its stream, and
+    then finishes its previous batch -- so every lane keeps two batches in
+    flight and the host work of one hides behind the GPU work of the other."""
 
-    def __init__(self, extractors, table, batches, cmn=True, ring=None, max_pending=None):
+    def __init__(self, extractors, table, batches, cmn=True):
         import torch
         self.torch = torch
         self.exs = list(extractors)
         self.table, self.cmn = table, cmn
         self.dev = torch.device("cuda", self.exs[0].device)
-        F = table.feat_dim
-        self.max_el = max((len(it) * L * F for L, it in batches), default=1)
-        self.max_n = max((len(it) for _, it in batches), default=1)
-        K = len(self.exs)
-        self.ring = ring or max(3, K + 2)
-        self.max_pending = max_pending or 2 * K + 2
-        dim = self.exs[0].dim
+        F, dim, K = table.feat_dim, self.exs[0].dim, len(self.exs)
+        max_el = max((len(it) * L * F for L, it in batches), default=1)
+        max_n = max((len(it) for _, it in batches), default=1)
+        self.threads = max(1, table.threads // K)
         self.streams = [torch.cuda.Stream(self.dev) for _ in range(K)]
-        self.d_in = [torch.empty(self.max_el, dtype=torch.float32, device=self.dev) for _ in range(K)]
-        self.d_out = [torch.empty(self.max_n * dim, dtype=torch.float32, device=self.dev)
+        self.d_in = [torch.empty(max_el, dtype=torch.float32, device=self.dev) for _ in range(K)]
+        self.d_out = [torch.empty(max_n * dim, dtype=torch.float32, device=self.dev) for _ in range(K)]
+        self.h_in = [[torch.empty(max_el, dtype=torch.float32).pin_memory() for _ in range(2)]
+                     for _ in range(K)]
+        self.h_out = [[torch.empty(max_n * dim, dtype=torch.float32).pin_memory() for _ in range(2)]
                       for _ in range(K)]
-        self.h_in = [torch.empty(self.max_el, dtype=torch.float32).pin_memory() for _ in range(self.ring)]
-        self.h_free = [None] * self.ring          # event after the H2D that last read h_in[k]
-        self.h_out = [torch.empty(self.max_n * dim, dtype=torch.float32).pin_memory()
-                      for _ in range(self.max_pending + 1)]
 
-    def run(self, batches):
-        torch = self.torch
-        K, F, dim = len(self.exs), self.table.feat_dim, self.exs[0].dim
-        pending = collections.deque()      # (bid, n, done event, h_out index)
-        reader = ThreadPoolExecutor(max_workers=1)
-        futs = {}
-
-        def submit(b):
-            k = b % self.ring
-            if self.h_free[k] is not None:
-                self.h_free[k].synchronize()
-            L, items = batches[b]
-            futs[b] = reader.submit(self.table.read, items, L, self.h_in[k], self.cmn)
-
+    def _lane(self, k, batches, results, stop):
+        torch, ex, s = self.torch, self.exs[k], self.streams[k]
+        F, dim = self.table.feat_dim, ex.dim
+        prev = None            # (bid, n, done event, pinned output)
+        free = [None, None]    # event after the H2D that last read h_in[k][j]
         try:
-            for b in range(min(self.ring - 1, len(batches))):
-                submit(b)
-            out_slot = 0
-            for b, (L, items) in enumerate(batches):
-                futs.pop(b).result()
-                if b + self.ring - 1 < len(batches):
-                    submit(b + self.ring - 1)
-                n, k, lane = len(items), b % self.ring, b % K
-                s = self.streams[lane]
-                ne = n * L * F
-                x = self.d_in[lane][:ne]
-                o = self.d_out[lane][:n * dim]
+            torch.cuda.set_device(self.dev)
+            for i, b in enumerate(range(k, len(batches), len(self.exs))):
+                if stop:
+                    return
+                L, items = batches[b]
+                n, j = len(items), i & 1
+                if free[j] is not None:
+                    free[j].synchronize()
+                hin = self.h_in[k][j]
+                self.table.read(items, L, hin, self.cmn, self.threads)
+                x, o = self.d_in[k][:n * L * F], self.d_out[k][:n * dim]
                 with torch.cuda.stream(s):
-                    x.copy_(self.h_in[k][:ne], non_blocking=True)
-                    ev = torch.cuda.Event()
-                    ev.record(s)
-                    self.h_free[k] = ev
-                self.exs[lane].run_device(x.view(n, L, F), o.view(n, dim), s)
-                while len(pending) >= self.max_pending:
-                    yield self._finish(pending.popleft())
-                h = self.h_out[out_slot]
-                out_slot = (out_slot + 1) % len(self.h_out)
+                    x.copy_(hin[:n * L * F], non_blocking=True)
+                    free[j] = torch.cuda.Event()
+                    free[j].record(s)
+                ex.run_device(x.view(n, L, F), o.view(n, dim), s)
+                h = self.h_out[k][j]
                 with torch.cuda.stream(s):
                     h[:n * dim].copy_(o, non_blocking=True)
                     done = torch.cuda.Event()
                     done.record(s)
-                pending.append((b, n, done, h))
-                while pending and pending[0][2].query():
-                    yield self._finish(pending.popleft())
-            while pending:
-                yield self._finish(pending.popleft())
+                if prev is not None:
+                    results.put(self._finish(prev, dim))
+                prev = (b, n, done, h)
+            if prev is not None:
+                results.put(self._finish(prev, dim))
+        except BaseException as e:   # surfaced by run() on the consuming thread
+            results.put(e)
         finally:
-            reader.shutdown(wait=True)
+            results.put(None)
 
-    def _finish(self, p):
+    @staticmethod
+    def _finish(p, dim):
         b, n, done, h = p
         done.synchronize()
-        dim = self.exs[0].dim
         return b, h[:n * dim].numpy().reshape(n, dim).copy()
+
+    def run(self, batches):
+        import queue
+        import threading
+        results, stop = queue.Queue(), []
+        lanes = [threading.Thread(target=self._lane, args=(k, batches, results, stop), daemon=True)
+                 for k in range(len(self.exs))]
+        for t in lanes:
+            t.start()
+        live, err = len(lanes), None
+        try:
+            while live:
+                r = results.get()
+                if r is None:
+                    live -= 1
+                elif isinstance(r, BaseException):
+                    err = err or r
+                    stop.append(1)
+                elif err is None:
+                    yield r
+        finally:
+            stop.append(1)
+            for t in lanes:
+                t.join()
+        if err is not None:
+            raise err
 
 
 def extract_stream(table, make_runner, batch=64):
