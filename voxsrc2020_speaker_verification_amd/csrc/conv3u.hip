@@ -163,9 +163,11 @@ __global__ __launch_bounds__(CU_NT) void conv3x3_utt(ConvParams p) {
     __syncthreads();
 
     int bb[CU_PG];
+    int tcol = col;
+    asm volatile("" : "+v"(tcol));   // (formed per tile, not hoisted out of the tile loop)
 #pragma unroll
     for (int j = 0; j < CU_PG; ++j) {
-      const int px = min(16 * (CU_PG * pg + j) + col, npx - 1);
+      const int px = min(16 * (CU_PG * pg + j) + tcol, npx - 1);
       const int slot = (px / W + 1) * SW + (px % W) + 1;
       bb[j] = cb + 32 * slot;
     }
@@ -198,10 +200,10 @@ __global__ __launch_bounds__(CU_NT) void conv3x3_utt(ConvParams p) {
       for (int part = 0; part < 6; ++part) {
         const int s = tap * 6 + part;
         __builtin_amdgcn_sched_barrier(0);
-        if (s > 0) {
-          if (s + 1 < CU_KS) cu_wait_vm<1>(); else cu_wait_vm<0>();
-          __syncthreads();   // step s landed for every wave; slot (s+2)%3 released
-        }
+        // (also at s = 0, where it is a no-op: a peeled first step spilled an
+        // accumulator through the whole first tap)
+        if (s + 1 < CU_KS) cu_wait_vm<1>(); else cu_wait_vm<0>();
+        __syncthreads();   // step s landed for every wave; slot (s+2)%3 released
         if (s + 2 < CU_KS) issue_w(s + 2);
         const char* L = ring + (s % CU_NST) * CU_WSLOT;
         bf16x8 a[3];
@@ -216,16 +218,22 @@ __global__ __launch_bounds__(CU_NT) void conv3x3_utt(ConvParams p) {
       }
     }
 
-    // ---- epilogue: lane (col, g) holds couts co .. co+3 of pixel 16 t + col
+    // ---- epilogue: lane (col, g) holds couts co .. co+3 of pixel 16 t + col.
+    // The lane indices are laundered here so the epilogue's addresses are
+    // formed after the k-loop: loop-invariant, they were hoisted out of the
+    // tile loop and held live across it (spilled: 92 / 76 B of scratch per lane)
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const int ecol = ln & 15, eg = ln >> 4;
     const size_t pbase = ((size_t)n * H + r0) * W;
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-      const int co = 48 * cg + 16 * i + 4 * g;
+      const int co = 48 * cg + 16 * i + 4 * eg;
       const f32x4 m = *reinterpret_cast<const f32x4*>(p.mean + co);
       const f32x4 iv = *reinterpret_cast<const f32x4*>(p.inv + co);
 #pragma unroll
       for (int j = 0; j < CU_PG; ++j) {
-        const int px = 16 * (CU_PG * pg + j) + col;
+        const int px = 16 * (CU_PG * pg + j) + ecol;
         if (px < npx) {
           bf16x4 o;
 #pragma unroll
