@@ -364,7 +364,8 @@ constexpr int GS_NL = 4;   // loader waves
 // then hold 96 accumulators and fit the cap; the residual takes 3 phases)
 // DBG (diagnostics, VOXEMB_GEMM_VAR 21/22): 1 = compute waves skip fragment
 // reads and MFMAs (stores kept), 2 = loaders issue no DMA, 8 = loaders skip
-// the weight pieces (operand + residual DMA only); results garbage
+// the weight pieces (operand + residual DMA only), 64 = no output stores,
+// 128 = loaders skip the residual pieces; results garbage
 // MODE (operand variants; 0 = the Res2Net 1x1s):
 //   GS_PRO : BN + ReLU prologue on the B operand, relu((x - m[k]) * inv[k])
 //            rounded to bf16, as gemm1x1_pipe<.., PRO> (DPN bn_relu_conv,
@@ -528,11 +529,11 @@ __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
           const int row = 2 * gi + (lane >> 5);
           const int c = (lane & 31) ^ (row & 15);
           const int pix = min(l_px0 + (BM / 4) * (gi >> 3) + 16 * ph + (row & 15), M - 1);
-          if (!(DBG & 2))
+          if (!(DBG & 2) && !(DBG & 128))
             gw_glds16(R + (size_t)pix * p.ldr + l_co0 + c * 8,
                       lds0 + (uint32_t)slot * GW_SLOT + (uint32_t)gi * 1024u);
         }
-        n = (DBG & 2) ? 0 : NLR;
+        n = ((DBG & 2) || (DBG & 128)) ? 0 : NLR;
       }
       if (l_k + 1 < SPT) {
         ++l_k;
@@ -651,7 +652,8 @@ __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
                             : (void*)(Y2 + (size_t)pix * p.ldy2 + (ch - p.ysplit));
       else
         dst = &g_gw_sink[lane];
-      gw_st16(dst, __builtin_bit_cast(u32x4, o));
+      if (DBG & 64) asm volatile("" ::"v"(o), "v"(dst));   // (diagnostics: no output stores)
+      else gw_st16(dst, __builtin_bit_cast(u32x4, o));
     }
   };
 
@@ -845,6 +847,9 @@ hipError_t launch_gemm_wide(const ConvParams& p0, int num_cu, int variant, hipSt
     else if (variant == 29) go(std::integral_constant<int, 9>{});
     else if (variant == 30) go(std::integral_constant<int, 16>{});
     else if (variant == 31) go(std::integral_constant<int, 32>{});
+    else if (variant == 26) go(std::integral_constant<int, 64>{});
+    else if (variant == 27) go(std::integral_constant<int, 65>{});
+    else if (variant == 23) go(std::integral_constant<int, 128>{});
     else
 #endif
       go(std::integral_constant<int, 0>{});
