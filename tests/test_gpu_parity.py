@@ -324,6 +324,30 @@ def test_gemm_ws_bitwise_wide(weights, name, F, T, N, var, monkeypatch):
     assert np.array_equal(got, ref)
 
 
+@pytest.mark.parametrize("name,F,T,N", [("tdnn", 80, 200, 64),
+                                        ("tdnn", 40, 123, 7),
+                                        ("res2net50_w24_s4_c32", 80, 200, 8),
+                                        ("res2net101_w24_s4_c32_att", 80, 64, 3)])
+def test_gemm_ws_two_ksteps_bitwise(weights, name, F, T, N, monkeypatch):
+    """gemm1x1_ws with two 32-deep k-steps per ring slot and barrier (the
+    128-pixel tiles of few-tile launches: the TDNN layers, small batches; the
+    default) gives the same bits as one k-step per slot (VOXEMB_GEMM_KSUB1=1)
+    on every layer output and the embeddings (the K order is unchanged)."""
+    import torch
+    from voxsrc2020_speaker_verification_amd import synth
+    spec, t, blob = weights(name, F)
+    x = synth.make_features(N, T, F, seed=61)
+    xd = torch.from_numpy(x).cuda()
+    with _extractor(blob, "bf16") as ex:
+        taps, emb = ex.layer_outputs(xd)
+    monkeypatch.setenv("VOXEMB_GEMM_KSUB1", "1")
+    with _extractor(blob, "bf16") as ex:
+        taps_1, emb_1 = ex.layer_outputs(xd)
+    for a, b in zip(taps, taps_1):
+        assert np.array_equal(a, b)
+    assert np.array_equal(emb, emb_1)
+
+
 @pytest.mark.parametrize("name,F,T,N", [("res2net50_w24_s4_c32", 80, 200, 16),
                                         ("res2net50_w24_s4_c32", 80, 123, 7),
                                         ("res2net50_w24_s4_c64", 40, 75, 3),

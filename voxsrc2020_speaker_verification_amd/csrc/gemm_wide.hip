@@ -376,10 +376,17 @@ constexpr int GS_NL = 4;   // loader waves
 //            chunk), B row of pixel (n, h) at tap t = input row h + t dh - ph of
 //            the same utterance, a zero row outside it (SAME padding)
 constexpr int GS_PRO = 1, GS_TAPS = 2;
-template <int BN, bool RES, int BM = GW_BM, int DBG = 0, int MODE = 0>
+// KSUB = 32-deep k-steps per ring slot and barrier: 1 (4 slots of 32 KB,
+// three in flight), or 2 for the 128-pixel tiles of the few-tile launches
+// (TDNN): 3 slots of 2 x (BN + BM) x 64 B, half the barrier-separated steps
+template <int BN, bool RES, int BM = GW_BM, int DBG = 0, int MODE = 0, int KSUB = 1>
 __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
   constexpr bool PRO = (MODE & GS_PRO) != 0, TAPS = (MODE & GS_TAPS) != 0;
   static_assert(!(PRO && TAPS), "one operand variant");
+  static_assert(KSUB == 1 || (KSUB == 2 && !RES && !PRO), "two k-steps per slot: plain or taps operands");
+  constexpr int SUBB = (BN + BM) * 64;                    // one k-step's operands
+  constexpr int SLOTB = KSUB == 1 ? GW_SLOT : KSUB * SUBB;
+  constexpr int NSTR = KSUB == 1 ? GW_NST : 3;
   constexpr int NI = BN / 32;
   constexpr int NQ = NI / 2;
   constexpr int NJ = BM / 64;                // 16-pixel columns per wave
@@ -404,7 +411,8 @@ __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
   const int M = p.N * p.Ho * p.Wo;
   const int HoWo = p.Ho * p.Wo;
   const int KT = p.kp / 32;
-  const int SPT = KT + NR;
+  const int KTS = KT / KSUB;          // ring steps of the K loop (the host checks KT % KSUB == 0)
+  const int SPT = KTS + NR;
   const int cblocks = p.coutp / BN;
   const int T = ((M + BM - 1) / BM) * cblocks;
   int t_first, t_step, ntiles;
@@ -433,7 +441,7 @@ __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
   const int flags = p.flags;
   const uint32_t lds0 = (uint32_t)(uintptr_t)smem;
 
-  float* tab = reinterpret_cast<float*>(smem + GW_NST * GW_SLOT);
+  float* tab = reinterpret_cast<float*>(smem + NSTR * SLOTB);
   if (flags & EPI_AFFINE) {
     for (int k = tid; k < p.coutp; k += GS_NT) {
       tab[k] = k < p.Cout ? p.mean[k] : 0.f;
@@ -499,30 +507,34 @@ __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
     auto issue = [&](int slot) -> int {
       int n = 0;
       if constexpr (PRO) {
-        const uint64_t v = l_k < KT ? (uint64_t)l_k : 0xFFFFull;
+        const uint64_t v = l_k < KTS ? (uint64_t)l_k : 0xFFFFull;
         kinfo = (kinfo & ~(0xFFFFull << (16 * slot))) | (v << (16 * slot));
       }
-      if (l_k < KT) {
-        // GS_TAPS: this k-step's tap and channel chunk (wave-uniform)
-        const int tap = TAPS ? (32 * l_k) / p.cinp : 0;
-        const int ci0 = TAPS ? 32 * l_k - tap * p.cinp : 0;
-        const int sh_t = TAPS ? tap * p.dh - p.ph : 0;
+      if (l_k < KTS) {
 #pragma unroll
-        for (int i = 0; i < NLL; ++i) {
-          const int gi = lw + GS_NL * i;
-          const int kst = i < BN / 64 ? wstep : 32;   // gi < BN/16 <=> i < BN/64
-          const bf16_t* a = src[i] + l_k * kst;
-          if (TAPS && i >= BN / 64) {
-            const int hi = tho[i] + sh_t;
-            a = (hi >= 0 && hi < p.H) ? src[i] + (size_t)hi * p.ldx + ci0 : zero;
+        for (int u = 0; u < KSUB; ++u) {
+          const int kk = l_k * KSUB + u;   // the k-step of sub-slot u
+          // GS_TAPS: this k-step's tap and channel chunk (wave-uniform)
+          const int tap = TAPS ? (32 * kk) / p.cinp : 0;
+          const int ci0 = TAPS ? 32 * kk - tap * p.cinp : 0;
+          const int sh_t = TAPS ? tap * p.dh - p.ph : 0;
+#pragma unroll
+          for (int i = 0; i < NLL; ++i) {
+            const int gi = lw + GS_NL * i;
+            const int kst = i < BN / 64 ? wstep : 32;   // gi < BN/16 <=> i < BN/64
+            const bf16_t* a = src[i] + kk * kst;
+            if (TAPS && i >= BN / 64) {
+              const int hi = tho[i] + sh_t;
+              a = (hi >= 0 && hi < p.H) ? src[i] + (size_t)hi * p.ldx + ci0 : zero;
+            }
+            if (!(DBG & 2) && !((DBG & 8) && i < BN / 64))
+              gw_glds16(a, lds0 + (uint32_t)slot * SLOTB + (uint32_t)(u * SUBB) + (uint32_t)gi * 1024u);
           }
-          if (!(DBG & 2) && !((DBG & 8) && i < BN / 64))
-            gw_glds16(a, lds0 + (uint32_t)slot * GW_SLOT + (uint32_t)gi * 1024u);
         }
-        n = (DBG & 2) ? 0 : (DBG & 8) ? NLL - BN / 64 : NLL;
+        n = KSUB * ((DBG & 2) ? 0 : (DBG & 8) ? NLL - BN / 64 : NLL);
       } else if (RES) {
         // residual phase ph: slot row r (512 B) = pixel l_px0 + (BM/4) (r / 16) + 16 ph + r % 16
-        const int ph = l_k - KT;
+        const int ph = l_k - KTS;
 #pragma unroll
         for (int i = 0; i < NLR; ++i) {
           const int gi = lw + GS_NL * i;
@@ -531,7 +543,7 @@ __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
           const int pix = min(l_px0 + (BM / 4) * (gi >> 3) + 16 * ph + (row & 15), M - 1);
           if (!(DBG & 2) && !(DBG & 128))
             gw_glds16(R + (size_t)pix * p.ldr + l_co0 + c * 8,
-                      lds0 + (uint32_t)slot * GW_SLOT + (uint32_t)gi * 1024u);
+                      lds0 + (uint32_t)slot * SLOTB + (uint32_t)gi * 1024u);
         }
         n = ((DBG & 2) || (DBG & 128)) ? 0 : NLR;
       }
@@ -546,7 +558,9 @@ __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
     };
     set_load_tile(0);
     issue(0);
-    int n1 = issue(1), n2 = issue(2);   // pieces of the two steps after the awaited one
+    // pieces of the NSTR - 2 steps after the awaited one (n1 unused with 3 slots)
+    int n1 = NSTR == 4 ? issue(1) : 0;
+    int n2 = issue(NSTR - 2);
     // GS_PRO: this lane's K chunk within a k-step (the DMA swizzle of an
     // activation row depends only on the lane: row = 16 gi + lane / 4)
     const int pc = (lane & 3) ^ ((4 - ((lane >> 4) & 3)) & 3);
@@ -569,7 +583,7 @@ __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
 #pragma unroll
           for (int i = BN / 64; i < NLL; ++i) {
             const int gi = lw + GS_NL * i;
-            bf16x8* q = reinterpret_cast<bf16x8*>(smem + slot * GW_SLOT + gi * 1024 + lane * 16);
+            bf16x8* q = reinterpret_cast<bf16x8*>(smem + slot * SLOTB + gi * 1024 + lane * 16);
             bf16x8 b = *q;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
@@ -583,8 +597,8 @@ __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
       }
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
-      const int n3 = issue((s + 3) & 3);
-      n1 = n2;
+      const int n3 = issue((s + NSTR - 1) % NSTR);
+      n1 = NSTR == 4 ? n2 : 0;
       n2 = n3;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -664,37 +678,41 @@ __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
     const int lid = t_first + c_tile * t_step;
     const int co0 = (lid % cblocks) * BN;
     const int px0 = (lid / cblocks) * BM;
-    const char* L = smem + (s & 3) * GW_SLOT;
-    if (c_k < KT && (DBG & 1)) {
-      if (!RES && c_k == KT - 1) {
+    const char* L = smem + (s % NSTR) * SLOTB;
+    if (c_k < KTS && (DBG & 1)) {
+      if (!RES && c_k == KTS - 1) {
         epi(std::integral_constant<int, 0>{}, co0, px0, nullptr);
         epi(std::integral_constant<int, 1>{}, co0, px0, nullptr);
         if constexpr (NJ > 2) epi(std::integral_constant<int, 2>{}, co0, px0, nullptr);
         if constexpr (NJ > 3) epi(std::integral_constant<int, 3>{}, co0, px0, nullptr);
       }
-    } else if (c_k < KT) {
-      // B fragments for the step, A fragments two cout blocks ahead (register budget)
-      bf16x8 a[NI], b[NJ];
+    } else if (c_k < KTS) {
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) b[j] = *reinterpret_cast<const bf16x8*>(L + offb + j * 1024);
-      // (GS_PRO: the loader waves applied the prologue to these fragments)
-      a[0] = *reinterpret_cast<const bf16x8*>(L + offa);
-      a[1] = *reinterpret_cast<const bf16x8*>(L + offa + 1024);
+      for (int u = 0; u < KSUB; ++u) {
+        const char* Lu = L + u * SUBB;
+        // B fragments for the k-step, A fragments two cout blocks ahead (register budget)
+        bf16x8 a[NI], b[NJ];
 #pragma unroll
-      for (int i = 0; i < NI; ++i) {
-        if (i + 2 < NI) a[i + 2] = *reinterpret_cast<const bf16x8*>(L + offa + (i + 2) * 1024);
+        for (int j = 0; j < NJ; ++j) b[j] = *reinterpret_cast<const bf16x8*>(Lu + offb + j * 1024);
+        // (GS_PRO: the loader waves applied the prologue to these fragments)
+        a[0] = *reinterpret_cast<const bf16x8*>(Lu + offa);
+        a[1] = *reinterpret_cast<const bf16x8*>(Lu + offa + 1024);
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) acc[i][j] = mfma_step(a[i], b[j], acc[i][j]);
-        __builtin_amdgcn_sched_barrier(0);
+        for (int i = 0; i < NI; ++i) {
+          if (i + 2 < NI) a[i + 2] = *reinterpret_cast<const bf16x8*>(Lu + offa + (i + 2) * 1024);
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) acc[i][j] = mfma_step(a[i], b[j], acc[i][j]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
       }
-      if (!RES && c_k == KT - 1) {
+      if (!RES && c_k == KTS - 1) {
         epi(std::integral_constant<int, 0>{}, co0, px0, nullptr);
         epi(std::integral_constant<int, 1>{}, co0, px0, nullptr);
         if constexpr (NJ > 2) epi(std::integral_constant<int, 2>{}, co0, px0, nullptr);
         if constexpr (NJ > 3) epi(std::integral_constant<int, 3>{}, co0, px0, nullptr);
       }
     } else if (RES) {
-      const int ph = c_k - KT;
+      const int ph = c_k - KTS;
       if (ph == 0) epi(std::integral_constant<int, 0>{}, co0, px0, L);
       else if (ph == 1) epi(std::integral_constant<int, 1>{}, co0, px0, L);
       else if (ph == 2) {
@@ -769,7 +787,7 @@ int gemm_wide_bm(const ConvParams& p0, int num_cu) {
   return bn == 320 ? 128 : ws_bm(p0.N * p0.Ho * p0.Wo, coutp / bn, bn, num_cu);
 }
 
-hipError_t launch_gemm_wide(const ConvParams& p0, int num_cu, int variant, hipStream_t s) {
+hipError_t launch_gemm_wide(const ConvParams& p0, int num_cu, int variant, hipStream_t s, int ksub_on) {
   const int bn = gemm_wide_bn(p0);
   if (!bn) return hipErrorInvalidValue;
   ConvParams p = p0;
@@ -788,6 +806,11 @@ hipError_t launch_gemm_wide(const ConvParams& p0, int num_cu, int variant, hipSt
     return g >= 8 ? g / 8 * 8 : g;
   };
   const int Gb = grid_for(bm);
+  // two k-steps per ring slot on the 128-pixel tiles (few-tile launches) when
+  // the three 2 x (BN + 128) x 64 B slots fit
+  const size_t lds2 = 3 * 2 * (size_t)(bn + 128) * 64 + 8 * (size_t)p.coutp;
+  const bool two = ksub_on && bm == 128 && bn <= 256 && !(p.flags & EPI_RES) && !p.in_mean &&
+                   (p.kp / 32) % 2 == 0 && lds2 <= 163840;
   if (p.in_mean || p.kh > 1) {
     // operand variants (GS_PRO / GS_TAPS): wave-specialised only
 #define WS_L(BN_, RES_, BM_, MODE_) \
@@ -802,6 +825,11 @@ hipError_t launch_gemm_wide(const ConvParams& p0, int num_cu, int variant, hipSt
       } else {
         if (bm == 128) WS_L(256, false, 128, GS_PRO); else WS_L(256, false, 192, GS_PRO);
       }
+    } else if (two) {
+      if (bn == 192)
+        hipLaunchKernelGGL((gemm1x1_ws<192, false, 128, 0, GS_TAPS, 2>), dim3(Gb), dim3(GS_NT), lds2, s, p);
+      else
+        hipLaunchKernelGGL((gemm1x1_ws<256, false, 128, 0, GS_TAPS, 2>), dim3(Gb), dim3(GS_NT), lds2, s, p);
     } else {
       if (bn == 192) {
         if (bm == 128) WS_L(192, false, 128, GS_TAPS); else WS_L(192, false, 256, GS_TAPS);
@@ -820,7 +848,11 @@ hipError_t launch_gemm_wide(const ConvParams& p0, int num_cu, int variant, hipSt
   if (variant == 1 || (variant >= 21 && variant <= 31)) {   // wave-specialised
     auto go = [&](auto dbgc) {
       constexpr int D = decltype(dbgc)::value;
-      if (bm == 128) {
+      if (two && bn == 192) {
+        hipLaunchKernelGGL((gemm1x1_ws<192, false, 128, 0, 0, 2>), dim3(Gb), dim3(GS_NT), lds2, s, p);
+      } else if (two) {
+        hipLaunchKernelGGL((gemm1x1_ws<256, false, 128, 0, 0, 2>), dim3(Gb), dim3(GS_NT), lds2, s, p);
+      } else if (bm == 128) {
         // too few tiles to fill the chip at the default size (small batches, TDNN)
         if (bn == 192)
           hipLaunchKernelGGL((gemm1x1_ws<192, false, 128, 0>), dim3(Gb), dim3(GS_NT), lds, s, p);
