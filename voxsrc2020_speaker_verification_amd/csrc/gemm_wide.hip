@@ -68,6 +68,9 @@ __device__ __forceinline__ void gw_st16(void* dst, u32x4 v) {
 __device__ __forceinline__ void gw_st16_nt(void* dst, u32x4 v) {
   asm volatile("global_store_dwordx4 %0, %1, off nt\n\ts_nop 1" : : "v"(dst), "v"(v) : "memory");
 }
+__device__ __forceinline__ void gw_st16_sc1(void* dst, u32x4 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" : : "v"(dst), "v"(v) : "memory");
+}
 
 #define GW_W(n) \
   case n: asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory"); break;
@@ -667,6 +670,8 @@ __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
       else
         dst = &g_gw_sink[lane];
       if (DBG & 64) asm volatile("" ::"v"(o), "v"(dst));   // (diagnostics: no output stores)
+      else if (DBG & 256) gw_st16_nt(dst, __builtin_bit_cast(u32x4, o));    // (nt stores)
+      else if (DBG & 512) gw_st16_sc1(dst, __builtin_bit_cast(u32x4, o));   // (sc1 stores)
       else gw_st16(dst, __builtin_bit_cast(u32x4, o));
     }
   };
@@ -845,7 +850,7 @@ hipError_t launch_gemm_wide(const ConvParams& p0, int num_cu, int variant, hipSt
   // VOXEMB_GEMM_VAR=-1 selects gemm1x1_wide
   if (variant == 0) variant = 1;
   if (variant == -1) variant = 0;
-  if (variant == 1 || (variant >= 21 && variant <= 31)) {   // wave-specialised
+  if (variant == 1 || (variant >= 21 && variant <= 34)) {   // wave-specialised
     auto go = [&](auto dbgc) {
       constexpr int D = decltype(dbgc)::value;
       if (two && bn == 192) {
@@ -882,6 +887,8 @@ hipError_t launch_gemm_wide(const ConvParams& p0, int num_cu, int variant, hipSt
     else if (variant == 26) go(std::integral_constant<int, 64>{});
     else if (variant == 27) go(std::integral_constant<int, 65>{});
     else if (variant == 23) go(std::integral_constant<int, 128>{});
+    else if (variant == 33) go(std::integral_constant<int, 256>{});
+    else if (variant == 34) go(std::integral_constant<int, 512>{});
     else
 #endif
       go(std::integral_constant<int, 0>{});
