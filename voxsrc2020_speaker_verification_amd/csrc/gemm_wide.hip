@@ -72,6 +72,21 @@ __device__ __forceinline__ void gw_st16_sc1(void* dst, u32x4 v) {
   asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" : : "v"(dst), "v"(v) : "memory");
 }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+// a - b on two lanes of a pair (v_pk_add_f32 with b negated: the rounding of two v_sub_f32)
+__device__ __forceinline__ f32x2 gw_pk_sub(f32x2 a, f32x2 b) {
+  f32x2 r;
+  asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+// max(0, v) as the one instruction fmaxf(v, 0.f) ends in (without its canonicalising
+// v_max_f32 v, v, v: the operands here are arithmetic results, never signalling NaNs)
+__device__ __forceinline__ float gw_relu(float v) {
+  float r;
+  asm("v_max_f32 %0, 0, %1" : "=v"(r) : "v"(v));
+  return r;
+}
+
 #define GW_W(n) \
   case n: asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory"); break;
 // s_waitcnt with a wave-uniform count (a scalar branch to the immediate form)
@@ -386,7 +401,7 @@ template <int BN, bool RES, int BM = GW_BM, int DBG = 0, int MODE = 0, int KSUB 
 __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
   constexpr bool PRO = (MODE & GS_PRO) != 0, TAPS = (MODE & GS_TAPS) != 0;
   static_assert(!(PRO && TAPS), "one operand variant");
-  static_assert(KSUB == 1 || (KSUB == 2 && !RES && !PRO), "two k-steps per slot: plain or taps operands");
+  static_assert(KSUB == 1 || (KSUB == 2 && !PRO), "two k-steps per slot: plain or taps operands");
   constexpr int SUBB = (BN + BM) * 64;                    // one k-step's operands
   constexpr int SLOTB = KSUB == 1 ? GW_SLOT : KSUB * SUBB;
   constexpr int NSTR = KSUB == 1 ? GW_NST : 3;
@@ -618,24 +633,33 @@ __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
   const int offa = (wm * (BN / 2) + col) * 64 + cs;
   const int offb = (BN + wn * (BM / 4) + col) * 64 + cs;
 
-  auto epi = [&](auto jc, int co0, int px0, const char* rl) {
+  // epilogue of one 16-pixel column J: FL = the EPI flags as a compile-time set for the
+  // common ones (-1 = read p.flags).  Packed pairs and a hoisted row address: the
+  // per-column VALU work, not the MFMAs, filled most of the residual phases.
+  auto epi_f = [&](auto jc, auto flc, int co0, int px0, const char* rl) {
     constexpr int J = decltype(jc)::value;
+    constexpr int FL = decltype(flc)::value;
+    const int fl = FL >= 0 ? FL : flags;
     const int pix = px0 + wn * (BM / 4) + 16 * J + col;
+    const bool pok = pix < M;
+    const int pixc = pok ? pix : M - 1;
+    bf16_t* const yrow = Y + (size_t)pixc * p.ldy;
+    const bool split = p.ysplit < p.Cout;   // two destinations (DPN dense channels)
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const int chl = wm * (BN / 2) + 32 * q + 8 * g;
       const int ch = co0 + chl;
-      float v[8];
+      f32x2 v[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        v[e] = acc[2 * q][J][e];
-        v[4 + e] = acc[2 * q + 1][J][e];
+      for (int e = 0; e < 2; ++e) {
+        v[e] = f32x2{acc[2 * q][J][2 * e], acc[2 * q][J][2 * e + 1]};
+        v[2 + e] = f32x2{acc[2 * q + 1][J][2 * e], acc[2 * q + 1][J][2 * e + 1]};
       }
-      if (flags & EPI_PRE_RELU) {
+      if (fl & EPI_PRE_RELU) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+        for (int e = 0; e < 4; ++e) v[e] = f32x2{gw_relu(v[e].x), gw_relu(v[e].y)};
       }
-      if (flags & EPI_AFFINE) {
+      if (fl & EPI_AFFINE) {
         // BN values re-read per column: not kept live across the 4 columns
         int tch = ch;
         asm volatile("" : "+v"(tch));
@@ -643,37 +667,54 @@ __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
         const f32x4 m1 = *reinterpret_cast<const f32x4*>(tab + tch + 4);
         const f32x4 i0 = *reinterpret_cast<const f32x4*>(tab + p.coutp + tch);
         const f32x4 i1 = *reinterpret_cast<const f32x4*>(tab + p.coutp + tch + 4);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          v[e] = (v[e] - m0[e]) * i0[e];
-          v[4 + e] = (v[4 + e] - m1[e]) * i1[e];
-        }
+        v[0] = gw_pk_sub(v[0], f32x2{m0[0], m0[1]}) * f32x2{i0[0], i0[1]};
+        v[1] = gw_pk_sub(v[1], f32x2{m0[2], m0[3]}) * f32x2{i0[2], i0[3]};
+        v[2] = gw_pk_sub(v[2], f32x2{m1[0], m1[1]}) * f32x2{i1[0], i1[1]};
+        v[3] = gw_pk_sub(v[3], f32x2{m1[2], m1[3]}) * f32x2{i1[2], i1[3]};
       }
-      if (RES && rl && ch < p.ysplit) {
+      if (RES && rl && (!split || ch < p.ysplit)) {
         const int row = wn * 16 + col;
-        const bf16x8 r8 = *reinterpret_cast<const bf16x8*>(
+        const u32x4 r4 = *reinterpret_cast<const u32x4*>(
             rl + row * 512 + ((((chl >> 3) ^ (row & 15))) << 4));
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] += (float)r8[e];
-      }
-      if (flags & EPI_RELU) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+        for (int e = 0; e < 4; ++e)
+          v[e] += f32x2{__builtin_bit_cast(float, r4[e] << 16), __builtin_bit_cast(float, r4[e] & 0xFFFF0000u)};
       }
       bf16x8 o;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = (bf16_t)v[e];
+      for (int e = 0; e < 4; ++e) {
+        o[2 * e] = (bf16_t)v[e].x;
+        o[2 * e + 1] = (bf16_t)v[e].y;
+      }
+      // relu(bf16(x)) == bf16(relu(x)) bit for bit (device_common.h)
+      if (fl & EPI_RELU) o = relu_bf16(o);
       void* dst;
-      if (ch < p.Cout && pix < M)
-        dst = ch < p.ysplit ? (void*)(Y + (size_t)pix * p.ldy + ch)
+      if (!split) {
+        dst = (ch < p.Cout && pok) ? (void*)(yrow + ch) : (void*)&g_gw_sink[lane];
+      } else if (ch < p.Cout && pok) {
+        dst = ch < p.ysplit ? (void*)(yrow + ch)
                             : (void*)(Y2 + (size_t)pix * p.ldy2 + (ch - p.ysplit));
-      else
+      } else {
         dst = &g_gw_sink[lane];
+      }
       if (DBG & 64) asm volatile("" ::"v"(o), "v"(dst));   // (diagnostics: no output stores)
       else if (DBG & 256) gw_st16_nt(dst, __builtin_bit_cast(u32x4, o));    // (nt stores)
       else if (DBG & 512) gw_st16_sc1(dst, __builtin_bit_cast(u32x4, o));   // (sc1 stores)
       else gw_st16(dst, __builtin_bit_cast(u32x4, o));
     }
+  };
+  // the flag sets of the Res2Net / TDNN / DPN 1x1s as compile-time epilogues
+  auto epi = [&](auto jc, int co0, int px0, const char* rl) {
+    using IC10 = std::integral_constant<int, EPI_AFFINE | EPI_RELU>;
+    using IC14 = std::integral_constant<int, EPI_AFFINE | EPI_RES | EPI_RELU>;
+    using IC2 = std::integral_constant<int, EPI_AFFINE>;
+    using IC3 = std::integral_constant<int, EPI_PRE_RELU | EPI_AFFINE>;
+    const int f = flags & (EPI_PRE_RELU | EPI_AFFINE | EPI_RES | EPI_RELU);
+    if (RES && f == (EPI_AFFINE | EPI_RES | EPI_RELU)) epi_f(jc, IC14{}, co0, px0, rl);
+    else if (!RES && f == (EPI_AFFINE | EPI_RELU)) epi_f(jc, IC10{}, co0, px0, rl);
+    else if (!RES && f == EPI_AFFINE) epi_f(jc, IC2{}, co0, px0, rl);
+    else if (!RES && f == (EPI_PRE_RELU | EPI_AFFINE)) epi_f(jc, IC3{}, co0, px0, rl);
+    else epi_f(jc, std::integral_constant<int, -1>{}, co0, px0, rl);
   };
 
   int c_tile = 0, c_k = 0;
@@ -792,7 +833,8 @@ int gemm_wide_bm(const ConvParams& p0, int num_cu) {
   return bn == 320 ? 128 : ws_bm(p0.N * p0.Ho * p0.Wo, coutp / bn, bn, num_cu);
 }
 
-hipError_t launch_gemm_wide(const ConvParams& p0, int num_cu, int variant, hipStream_t s, int ksub_on) {
+hipError_t launch_gemm_wide(const ConvParams& p0, int num_cu, int variant, hipStream_t s, int ksub_on,
+                             int force_bm) {
   const int bn = gemm_wide_bn(p0);
   if (!bn) return hipErrorInvalidValue;
   ConvParams p = p0;
@@ -804,7 +846,7 @@ hipError_t launch_gemm_wide(const ConvParams& p0, int num_cu, int variant, hipSt
   G = G >= 8 ? G / 8 * 8 : G;   // small launches (any_m) keep their few tiles
   const size_t lds = GW_NST * GW_SLOT + 8 * (size_t)p.coutp + (p.in_mean ? 8 * (size_t)p.kp : 0);
   // (the 320-wide tile holds 80 accumulators per compute wave at 128 pixels)
-  const int bm = bn == 320 ? 128 : ws_bm(M, p.coutp / bn, bn, num_cu);
+  const int bm = bn == 320 || (force_bm == 128 && !p.in_mean) ? 128 : ws_bm(M, p.coutp / bn, bn, num_cu);
   auto grid_for = [&](int bmx) {
     const int t = ((M + bmx - 1) / bmx) * (p.coutp / bn);
     int g = num_cu < t ? num_cu : t;
@@ -814,7 +856,7 @@ hipError_t launch_gemm_wide(const ConvParams& p0, int num_cu, int variant, hipSt
   // two k-steps per ring slot on the 128-pixel tiles (few-tile launches) when
   // the three 2 x (BN + 128) x 64 B slots fit
   const size_t lds2 = 3 * 2 * (size_t)(bn + 128) * 64 + 8 * (size_t)p.coutp;
-  const bool two = ksub_on && bm == 128 && bn <= 256 && !(p.flags & EPI_RES) && !p.in_mean &&
+  const bool two = ksub_on && bm == 128 && bn <= 256 && !p.in_mean &&
                    (p.kp / 32) % 2 == 0 && lds2 <= 163840;
   if (p.in_mean || p.kh > 1) {
     // operand variants (GS_PRO / GS_TAPS): wave-specialised only
@@ -855,6 +897,8 @@ hipError_t launch_gemm_wide(const ConvParams& p0, int num_cu, int variant, hipSt
       constexpr int D = decltype(dbgc)::value;
       if (two && bn == 192) {
         hipLaunchKernelGGL((gemm1x1_ws<192, false, 128, 0, 0, 2>), dim3(Gb), dim3(GS_NT), lds2, s, p);
+      } else if (two && (p.flags & EPI_RES)) {
+        hipLaunchKernelGGL((gemm1x1_ws<256, true, 128, 0, 0, 2>), dim3(Gb), dim3(GS_NT), lds2, s, p);
       } else if (two) {
         hipLaunchKernelGGL((gemm1x1_ws<256, false, 128, 0, 0, 2>), dim3(Gb), dim3(GS_NT), lds2, s, p);
       } else if (bm == 128) {
