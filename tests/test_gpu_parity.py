@@ -425,6 +425,31 @@ def test_gemm_pipe_prologue_bitwise(weights, F, T, N, monkeypatch):
 
 
 @pytest.mark.parametrize("F,T,N", [(80, 64, 2), (40, 97, 3), (80, 33, 5)])
+def test_smallk_v2_bitwise_v1(weights, F, T, N, monkeypatch):
+    """DPN68's two 10-channel 1x1s (the stem output's projection and 1x1a, BN +
+    ReLU prologue) on conv1x1_smallk2 -- prologue staged once per pixel in LDS,
+    packed fma pairs -- give the same bits as conv1x1_smallk (version 1): every
+    tap and the embeddings, pixel counts ragged against the 128-pixel pass."""
+    import torch
+    from voxsrc2020_speaker_verification_amd import synth
+    spec, t, blob = weights("dpn68", F)
+    x = synth.make_features(N, T, F, seed=29)
+    with _extractor(blob, "bf16") as ex:
+        xd = torch.from_numpy(x).cuda()
+        got = ex.run(x)
+        taps_got, _ = ex.layer_outputs(xd)
+        assert len([l for l in ex.describe(xd) if l.startswith("smallk ")]) == 2
+    monkeypatch.setenv("VOXEMB_SMALLK_V1", "1")
+    with _extractor(blob, "bf16") as ex:
+        xd = torch.from_numpy(x).cuda()
+        ref = ex.run(x)
+        taps_ref, _ = ex.layer_outputs(xd)
+    for i, (a, b) in enumerate(zip(taps_got, taps_ref)):
+        assert np.array_equal(a, b), f"tap {i}"
+    assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("F,T,N", [(80, 64, 2), (40, 97, 3), (80, 33, 5)])
 def test_conv1x1_nw_bitwise_rr(weights, F, T, N, monkeypatch):
     """DPN68's narrow 1x1s (K <= 256, <= 192 couts) on the LDS-resident-weight
     GEMM (prologue in registers, residual below ysplit, dense channels past it,

@@ -288,6 +288,7 @@ struct vox_model {
   int no_gemm_pro = 0;     // VOXEMB_NO_GEMM_PRO: prologue 1x1 convs off the LDS-DMA GEMMs
   int no_gemm_taps = 0;    // VOXEMB_NO_GEMM_TAPS: TDNN dilated convs off gemm1x1_ws
   int no_smallk = 0;       // VOXEMB_NO_SMALLK: DPN 10-channel 1x1s on the generic conv
+  int smallk_v1 = 0;       // VOXEMB_SMALLK_V1: conv1x1_smallk (version 1) instead of version 2
   int no_nw = 0;           // VOXEMB_NO_NW: narrow 1x1s on conv1x1_rr instead of conv1x1_nw
   int no_dpn_block = 0;    // VOXEMB_NO_DPN_BLOCK: DPN stage-1 blocks as 1x1a / gconv / 1x1c launches
   int dpn_nseg = 0;        // VOXEMB_DPN_NSEG: force dpn_block_rows' segments per utterance (tests)
@@ -297,6 +298,7 @@ struct vox_model {
   int gemm_ksub1 = 0;      // VOXEMB_GEMM_KSUB1: gemm1x1_ws's 128-pixel tiles with one k-step
                            // per ring slot instead of two (bitwise A/B)
   int gemm_bm = 0;         // VOXEMB_GEMM_BM: 128 = gemm1x1_ws's 128-pixel tiles on every launch
+  int gemm_bk64 = 0;       // VOXEMB_GEMM_BK64: gemm1x1_ws 64-deep steps on the 448-row tiles
   int gemm_var = 0;        // VOXEMB_GEMM_VAR: -1 = gemm1x1_wide instead of gemm1x1_ws
                            // (bitwise A/B); other values are diagnostics (VOX_DIAG builds)
   int gemm_min_k = 128;    // VOXEMB_GEMM_MIN_K: smallest K routed to the LDS GEMMs (the K = 128
@@ -334,6 +336,7 @@ static const PlanEnv kPlanEnv[] = {
     {"VOXEMB_NO_GEMM_PRO", &vox_model::no_gemm_pro},
     {"VOXEMB_NO_GEMM_TAPS", &vox_model::no_gemm_taps},
     {"VOXEMB_NO_SMALLK", &vox_model::no_smallk},
+    {"VOXEMB_SMALLK_V1", &vox_model::smallk_v1},
     {"VOXEMB_NO_NW", &vox_model::no_nw},
     {"VOXEMB_NO_DPN_BLOCK", &vox_model::no_dpn_block},
     {"VOXEMB_DPN_NSEG", &vox_model::dpn_nseg},
@@ -343,6 +346,7 @@ static const PlanEnv kPlanEnv[] = {
     {"VOXEMB_GEMM_VAR", &vox_model::gemm_var},
     {"VOXEMB_GEMM_KSUB1", &vox_model::gemm_ksub1},
     {"VOXEMB_GEMM_BM", &vox_model::gemm_bm},
+    {"VOXEMB_GEMM_BK64", &vox_model::gemm_bk64},
     {"VOXEMB_GEMM_MIN_K", &vox_model::gemm_min_k},
     {"VOXEMB_NO_CHAIN", &vox_model::no_chain},
     {"VOXEMB_NO_STEM", &vox_model::no_stem},
@@ -1742,7 +1746,7 @@ static hipError_t run_op(vox_model* m, const Op& op, hipStream_t s) {
     case 18: return launch_gemm_pipe(op.cp, m->num_cu, m->gemm_var, s);
     case 19: return launch_gconv(op.gq, s);
     case 20: return launch_conv3_pipe(op.cp, m->num_cu, s);
-    case 21: return launch_gemm_wide(op.cp, m->num_cu, m->gemm_var, s, !m->gemm_ksub1, m->gemm_bm);
+    case 21: return launch_gemm_wide(op.cp, m->num_cu, m->gemm_var, s, !m->gemm_ksub1, m->gemm_bm, m->gemm_bk64);
     case 10: return launch_split_chain(op.ch, op.cl.wco, op.cl.wpx, s);
     case 12: return launch_bneck(op.bq, op.cin, op.C, op.cl.wco, op.S, s);
     case 13: return launch_chain_rows(op.ch, s);
@@ -1754,7 +1758,7 @@ static hipError_t run_op(vox_model* m, const Op& op, hipStream_t s) {
     case 31: return launch_dpn_block(op.dq, s);
     case 32: return launch_dpn_down(op.ddq, s);
     case 26: return launch_conv3_utt(op.cp, m->num_cu, s);
-    case 27: return launch_conv1x1_smallk(op.cp, s);
+    case 27: return launch_conv1x1_smallk(op.cp, s, m->smallk_v1);
     case 29: return launch_conv1x1_nw(op.cp, m->num_cu, s);
     case 28: return launch_conv3_s2r(op.cp, m->num_cu, s);
     case 15: return launch_convert_bf16(op.src, (float*)op.dst, op.count, s);

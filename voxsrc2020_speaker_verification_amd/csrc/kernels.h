@@ -170,7 +170,7 @@ int gemm_wide_bm(const ConvParams& p, int num_cu);
 // ksub_on: gemm1x1_ws's 128-pixel tiles take two 32-deep k-steps per ring slot
 // and barrier where they fit (bitwise the same outputs)
 hipError_t launch_gemm_wide(const ConvParams& p, int num_cu, int variant, hipStream_t s, int ksub_on = 1,
-                             int force_bm = 0);
+                             int force_bm = 0, int bk64 = 0);
 // Persistent LDS-DMA pipelined 3x3 implicit GEMM (conv3.hip) for the Res2Net
 // branch convs with Cin in {96, 192}: stride 1 (SAME) or 2 (fixed pad 1),
 // Cout % 96 == 0, epilogue BN + ReLU; with y2 set (stride 1) it also writes
@@ -253,7 +253,7 @@ hipError_t launch_dpn_block(const DpnBlockParams& p, hipStream_t s);
 
 // DPN68's 10-channel 1x1 convs with the BN+ReLU prologue (kernels.hip)
 int conv1x1_smallk_ok(const ConvParams& p);
-hipError_t launch_conv1x1_smallk(const ConvParams& p, hipStream_t s);
+hipError_t launch_conv1x1_smallk(const ConvParams& p, hipStream_t s, int v1 = 0);
 
 hipError_t launch_splitk_reduce(const float* partial, int S, int M, int coutp, int cout,
                                 const float* mean, const float* inv, int flags,

@@ -1985,6 +1985,110 @@ __global__ __launch_bounds__(256) void conv1x1_smallk(ConvParams p) {
   }
 }
 
+// Version 2 (the product kernel; version 1 above behind VOXEMB_SMALLK_V1, bitwise
+// equal): version 1 ran at 2.8 TB/s, instruction-bound -- each of the Cout / 8
+// threads of a pixel re-loaded its 10 inputs and re-ran their BN + ReLU prologue
+// (about 140 VALU per thread-pixel).  Here a workgroup pass of SMALLK_PX x
+// SMALLK_PXU pixels first stages the pass's prologued inputs once (thread = one
+// (pixel, channel pair), the fixed pair's mean / inverse in registers) as fp32
+// rows in LDS, then every thread reads its pixel's row back (LDS broadcast) and
+// runs the same fma chain, k = 0..K-1 in order, on packed pairs of output
+// channels (v_pk_fma_f32: per element the same rounding as the scalar chain).
+constexpr int SMALLK_ROW = 12;   // floats per staged pixel row (K = 10, 16-B aligned rows)
+template <int K, int NC>
+__global__ __launch_bounds__(256) void conv1x1_smallk2(ConvParams p) {
+  static_assert(K % 2 == 0 && K <= SMALLK_ROW, "dword input loads, one staged row");
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  constexpr int PASS = SMALLK_PX * SMALLK_PXU;
+  constexpr int NT = SMALLK_PX * NC;    // threads (Cout = 8 NC)
+  __shared__ __attribute__((aligned(16))) float xs[PASS * SMALLK_ROW];
+  const int tid = threadIdx.x;
+  const int c = tid % NC, pl = tid / NC;
+  const int co = 8 * c;
+  const bf16_t* __restrict__ Wt = reinterpret_cast<const bf16_t*>(p.w);
+  f32x2 w[4][K];   // output channel pairs (co + 2h, co + 2h + 1)
+#pragma unroll
+  for (int h = 0; h < 4; ++h)
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      w[h][k] = f32x2{(float)Wt[(size_t)(co + 2 * h) * p.kp + k], (float)Wt[(size_t)(co + 2 * h + 1) * p.kp + k]};
+  // staging role: thread -> channel pair kq (fixed), pixels sp0 + i SPP of the pass
+  constexpr int KQ = K / 2;
+  constexpr int SPP = NT / KQ;                  // pixels staged per sweep
+  constexpr int NS = (PASS + SPP - 1) / SPP;    // sweeps per pass
+  const int kq = tid % KQ, sp0 = tid / KQ;
+  const bool stager = sp0 < SPP;
+  float bm0 = 0.f, bm1 = 0.f, bi0 = 1.f, bi1 = 1.f;
+  if (p.in_mean) {
+    bm0 = p.in_mean[2 * kq]; bm1 = p.in_mean[2 * kq + 1];
+    bi0 = p.in_inv[2 * kq]; bi1 = p.in_inv[2 * kq + 1];
+  }
+  const int64_t npx = (int64_t)p.N * p.H * p.W;
+  const bf16_t* __restrict__ X0 = reinterpret_cast<const bf16_t*>(p.x);
+  bf16_t* Y = reinterpret_cast<bf16_t*>(p.y);
+  bf16_t* Y2 = reinterpret_cast<bf16_t*>(p.y2);
+  const bool lo = co < p.ysplit;
+  const int64_t gstep = (int64_t)gridDim.x * PASS;
+  // the next pass's inputs are requested before this pass's outputs are computed
+  unsigned raw[NS];
+  auto fetch = [&](int64_t base) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      const int sp = sp0 + i * SPP;
+      const int64_t pix = base + sp;
+      raw[i] = (stager && sp < PASS && pix < npx)
+                   ? *reinterpret_cast<const unsigned*>(X0 + pix * p.ldx + 2 * kq) : 0u;
+    }
+  };
+  int64_t base = (int64_t)blockIdx.x * PASS;
+  if (base < npx) fetch(base);
+  for (; base < npx; base += gstep) {
+    if (stager) {
+#pragma unroll
+      for (int i = 0; i < NS; ++i) {
+        const int sp = sp0 + i * SPP;
+        if (sp >= PASS) break;
+        float v0 = __builtin_bit_cast(float, raw[i] << 16);
+        float v1 = __builtin_bit_cast(float, raw[i] & 0xFFFF0000u);
+        if (p.in_mean) {
+          v0 = fmaxf((v0 - bm0) * bi0, 0.f);
+          v1 = fmaxf((v1 - bm1) * bi1, 0.f);
+        }
+        // the bf16 operand the MFMA paths feed
+        *reinterpret_cast<f32x2*>(&xs[sp * SMALLK_ROW + 2 * kq]) = f32x2{(float)(bf16_t)v0, (float)(bf16_t)v1};
+      }
+    }
+    __syncthreads();
+    if (base + gstep < npx) fetch(base + gstep);
+#pragma unroll 2
+    for (int u = 0; u < SMALLK_PXU; ++u) {
+      const int sp = pl + SMALLK_PX * u;
+      const int64_t pix = base + sp;
+      if (pix >= npx) break;
+      float xv[SMALLK_ROW];
+      *reinterpret_cast<f32x4*>(&xv[0]) = *reinterpret_cast<const f32x4*>(&xs[sp * SMALLK_ROW]);
+      *reinterpret_cast<f32x4*>(&xv[4]) = *reinterpret_cast<const f32x4*>(&xs[sp * SMALLK_ROW + 4]);
+      *reinterpret_cast<f32x4*>(&xv[8]) = *reinterpret_cast<const f32x4*>(&xs[sp * SMALLK_ROW + 8]);
+      f32x2 acc[4];
+#pragma unroll
+      for (int h = 0; h < 4; ++h) acc[h] = f32x2{0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < K; ++k)
+#pragma unroll
+        for (int h = 0; h < 4; ++h) acc[h] = __builtin_elementwise_fma(f32x2{xv[k], xv[k]}, w[h][k], acc[h]);
+      bf16x8 o;
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        o[2 * h] = (bf16_t)acc[h][0];
+        o[2 * h + 1] = (bf16_t)acc[h][1];
+      }
+      bf16_t* dst = lo ? Y + pix * p.ldy + co : Y2 + pix * p.ldy2 + (co - p.ysplit);
+      *reinterpret_cast<uint4*>(dst) = __builtin_bit_cast(uint4, o);
+    }
+    __syncthreads();
+  }
+}
+
 int conv1x1_smallk_ok(const ConvParams& p) {
   return p.kh == 1 && p.kw == 1 && p.sh == 1 && p.sw == 1 && p.ph == 0 && p.pw == 0 &&
          p.groups == 1 && p.Cin == 10 && p.Cout % 8 == 0 && p.Cout <= 128 && p.flags == 0 &&
@@ -1993,13 +2097,20 @@ int conv1x1_smallk_ok(const ConvParams& p) {
          p.Ho == p.H && p.Wo == p.W && p.ldx % 2 == 0 && (uintptr_t)p.x % 4 == 0;
 }
 
-hipError_t launch_conv1x1_smallk(const ConvParams& p, hipStream_t s) {
+hipError_t launch_conv1x1_smallk(const ConvParams& p, hipStream_t s, int v1) {
   if (!conv1x1_smallk_ok(p)) return hipErrorInvalidValue;
   const int64_t n = (int64_t)p.N * p.H * p.W;
   const int64_t blocks = (n + SMALLK_PX * SMALLK_PXU - 1) / (SMALLK_PX * SMALLK_PXU);
   // a few passes per workgroup (the weight loads amortised)
   const unsigned G = (unsigned)(blocks < 4096 ? blocks : 4096);
-  hipLaunchKernelGGL((conv1x1_smallk<10>), dim3(G), dim3(SMALLK_PX * (p.Cout / 8)), 0, s, p);
+  if (v1)
+    hipLaunchKernelGGL((conv1x1_smallk<10>), dim3(G), dim3(SMALLK_PX * (p.Cout / 8)), 0, s, p);
+  else if (p.Cout == 96)
+    hipLaunchKernelGGL((conv1x1_smallk2<10, 12>), dim3(G), dim3(SMALLK_PX * 12), 0, s, p);
+  else if (p.Cout == 128)
+    hipLaunchKernelGGL((conv1x1_smallk2<10, 16>), dim3(G), dim3(SMALLK_PX * 16), 0, s, p);
+  else
+    hipLaunchKernelGGL((conv1x1_smallk<10>), dim3(G), dim3(SMALLK_PX * (p.Cout / 8)), 0, s, p);
   return hipGetLastError();
 }
 }  // namespace vox
