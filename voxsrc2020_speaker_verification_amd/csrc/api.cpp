@@ -2091,6 +2091,13 @@ extern "C" int vox_debug_bneck_trace(void* dst, size_t bytes) {
   return VOX_OK;
 }
 
+// diagnostics: conv3x3_ks clock stamps (12 waves x 16 tiles x 8 u64), see conv3k.hip
+extern "C" int vox_debug_ks_trace(void* dst, size_t bytes) {
+  if (!dst) return fail(VOX_EINVAL, "null argument");
+  HIPCHK(ks_trace_read(dst, bytes));
+  return VOX_OK;
+}
+
 extern "C" int vox_plan_describe(vox_model* m, const float* d_x, int n, int t, int f, char* buf,
                                  size_t cap) {
   if (!m || !d_x) return fail(VOX_EINVAL, "null argument");

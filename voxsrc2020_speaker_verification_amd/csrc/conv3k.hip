@@ -56,6 +56,13 @@ constexpr int KS_XCH = KS_NW * 4096;   // partial-sum exchange: 4 KB per wave
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+// a - b on a pair (v_pk_add_f32, b negated: the rounding of two v_sub_f32)
+__device__ __forceinline__ f32x2 ks_pk_sub(f32x2 a, f32x2 b) {
+  f32x2 r;
+  asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
 
 __device__ __forceinline__ void ks_glds16(const void* src, uint32_t lds) {
   unsigned keep;
@@ -80,6 +87,9 @@ __device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
 }  // namespace
 
 __device__ uint4 g_ks_zero[4] = {};
+// diagnostics (libvoxemb_diag.so only): shader-clock stamps of workgroup 0 of
+// the z-forming launches, [wave][tile < 16][stamp < 8] (tools/ks_trace.py)
+__device__ unsigned long long g_ks_trace[KS_NW * 16 * 8];
 __device__ uint4 g_ks_sink[64];   // destination of masked lanes' stores
 
 template <int W>
@@ -153,22 +163,23 @@ __global__ __launch_bounds__(KS_NT) void conv3x3_ks(ConvParams p) {
 
   // window piece q of tile tj into buffer b: units [64q, 64q + 64), unit u =
   // chunk u % 13 of slot u / 13 (chunk 12 = the pad unit)
+  auto issue_piece = [&](int n, int r0w, int b, int q) __attribute__((always_inline)) {
+    int u = lane;
+    asm volatile("" : "+v"(u));
+    u += 64 * q;
+    const int x = u / KS_PU, c = u - x * KS_PU;
+    const int rr = x / SW, sc = x - rr * SW;
+    const int row = r0w + rr;
+    const bf16_t* src = zero;
+    if (c < KS_NCH && sc > 0 && rr < K::RMAX && row >= 0 && row < H)
+      src = X + ((size_t)n * HW + row * W + (sc - 1)) * p.ldx + c * 8;
+    ks_glds16(src, lds0 + (uint32_t)b * K::WBUF + (uint32_t)q * 1024u);
+  };
   auto issue_win = [&](int tj, int b) __attribute__((always_inline)) {
     const int id = t_first + tj * t_step;
     const int n = id / tpu, t = id - n * tpu;
     const int r0w = (t * KS_TP) / W - 1;   // image row of window row 0
-    for (int q = wave; q < K::WPC; q += KS_NW) {
-      int u = lane;
-      asm volatile("" : "+v"(u));
-      u += 64 * q;
-      const int x = u / KS_PU, c = u - x * KS_PU;
-      const int rr = x / SW, sc = x - rr * SW;
-      const int row = r0w + rr;
-      const bf16_t* src = zero;
-      if (c < KS_NCH && sc > 0 && rr < K::RMAX && row >= 0 && row < H)
-        src = X + ((size_t)n * HW + row * W + (sc - 1)) * p.ldx + c * 8;
-      ks_glds16(src, lds0 + (uint32_t)b * K::WBUF + (uint32_t)q * 1024u);
-    }
+    for (int q = wave; q < K::WPC; q += KS_NW) issue_piece(n, r0w, b, q);
   };
 
   // the tile's x_{k+1} pixel rows (192 B each) into LDS, linear
@@ -201,10 +212,37 @@ __global__ __launch_bounds__(KS_NT) void conv3x3_ks(ConvParams p) {
   // partial of group 2 ph + (1 - kh) to its partner (cg, 1 - kh, ph)
   const int gown = 2 * ph + kh, gpart = 2 * ph + (1 - kh);
   const int partner = cg + 3 * (1 - kh) + 6 * ph;
+#ifdef VOX_DIAG
+  const bool trace = HAS_Z && blockIdx.x == 0 && lane == 0;
+#else
+  constexpr bool trace = false;
+#endif
+  auto stamp = [&](int tj, int i) __attribute__((always_inline)) {
+    if (trace && tj < 16) g_ks_trace[(wave * 16 + tj) * 8 + i] = __builtin_amdgcn_s_memtime();
+  };
   for (int tj = 0; tj < ntiles; ++tj) {
     const int b = tj & 1;
+    stamp(tj, 0);
     if (HAS_Z) issue_xz(tj);
-    if (tj + 1 < ntiles) issue_win(tj + 1, b ^ 1);
+    // the next tile's window pieces go out between the first pass's MFMAs
+    // (issued together here they held every wave ~2-4k clk per tile before
+    // its first MFMA; conv3x3_ks 990 -> 967 us per step); same issue order
+    // relative to the x rows and stores
+    int n1 = 0, r0w1 = 0;
+    const bool more = tj + 1 < ntiles;
+    if (more) {
+      const int id1 = t_first + (tj + 1) * t_step;
+      n1 = id1 / tpu;
+      r0w1 = ((id1 - n1 * tpu) * KS_TP) / W - 1;
+    }
+    auto fill = [&](int s) __attribute__((always_inline)) {
+      if (more && s % 6 == 3) {
+        const int q = wave + KS_NW * (s / 6);
+        if (q < K::WPC) issue_piece(n1, r0w1, b ^ 1, q);
+      }
+    };
+    auto nofill = [](int) {};
+    stamp(tj, 1);
     const int id = t_first + tj * t_step;
     const int n = id / tpu, t = id - n * tpu;
     const int p0 = t * KS_TP;
@@ -227,7 +265,7 @@ __global__ __launch_bounds__(KS_NT) void conv3x3_ks(ConvParams p) {
     // one pass: the 27 k16-steps of K half KH over pixel group j, one
     // accumulation chain (32x32x16 needs no interleaving for throughput),
     // fragments read two steps ahead
-    auto kpass = [&](auto khc, int j) __attribute__((always_inline)) {
+    auto kpass = [&](auto khc, int j, auto&& fl) __attribute__((always_inline)) {
       constexpr int KH = decltype(khc)::value;
       auto off = [](int s) constexpr {
         const int S = 27 * KH + s, tap = S / 6, part = S % 6;
@@ -247,34 +285,42 @@ __global__ __launch_bounds__(KS_NT) void conv3x3_ks(ConvParams p) {
         if (s + 2 < KS_SH) bf[(s + 2) % 3] = *reinterpret_cast<const bf16x8*>(smem + bs + off(s + 2));
         __builtin_amdgcn_sched_barrier(0);
         acc = mfma32(wr[s], bf[s % 3], acc);
+        fl(s);
         __builtin_amdgcn_sched_barrier(0);
       }
       return acc;
     };
     f32x16 acc;
     if (kh == 0) {
-      const f32x16 give = kpass(std::integral_constant<int, 0>{}, gpart);
+      const f32x16 give = kpass(std::integral_constant<int, 0>{}, gpart, fill);
 #pragma unroll
       for (int r4 = 0; r4 < 4; ++r4)
         *reinterpret_cast<f32x4*>(xch + wave * 1024 + r4 * 256 + ln * 4) =
             f32x4{give[4 * r4], give[4 * r4 + 1], give[4 * r4 + 2], give[4 * r4 + 3]};
-      acc = kpass(std::integral_constant<int, 0>{}, gown);
+      stamp(tj, 2);
+      acc = kpass(std::integral_constant<int, 0>{}, gown, nofill);
     } else {
-      const f32x16 give = kpass(std::integral_constant<int, 1>{}, gpart);
+      const f32x16 give = kpass(std::integral_constant<int, 1>{}, gpart, fill);
 #pragma unroll
       for (int r4 = 0; r4 < 4; ++r4)
         *reinterpret_cast<f32x4*>(xch + wave * 1024 + r4 * 256 + ln * 4) =
             f32x4{give[4 * r4], give[4 * r4 + 1], give[4 * r4 + 2], give[4 * r4 + 3]};
-      acc = kpass(std::integral_constant<int, 1>{}, gown);
+      stamp(tj, 2);
+      acc = kpass(std::integral_constant<int, 1>{}, gown, nofill);
     }
+    stamp(tj, 3);
     // this tile's x rows have landed: younger are the next window's pieces
     if (HAS_Z) vm_wait(tj + 1 < ntiles ? nwin : 0);
+    stamp(tj, 4);
     __syncthreads();   // B: partials and x rows visible; every wave done with window b
+    stamp(tj, 5);
+    // (half 0) + (half 1), BN on packed pairs (the same roundings as scalar)
+    f32x2 a2[8];
 #pragma unroll
     for (int r4 = 0; r4 < 4; ++r4) {
       const f32x4 v = *reinterpret_cast<const f32x4*>(xch + partner * 1024 + r4 * 256 + ln * 4);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) acc[4 * r4 + e] = acc[4 * r4 + e] + v[e];   // (half 0) + (half 1)
+      a2[2 * r4] = f32x2{acc[4 * r4], acc[4 * r4 + 1]} + f32x2{v[0], v[1]};
+      a2[2 * r4 + 1] = f32x2{acc[4 * r4 + 2], acc[4 * r4 + 3]} + f32x2{v[2], v[3]};
     }
     // y: register group q holds couts 32 cg + 8 q + 4 h + (0..3) of pixel pxo
     unsigned yd[4][2];
@@ -283,9 +329,11 @@ __global__ __launch_bounds__(KS_NT) void conv3x3_ks(ConvParams p) {
       const int co = 32 * cg + 8 * q + 4 * h;
       const f32x4 m = *reinterpret_cast<const f32x4*>(bnm + co);
       const f32x4 iv = *reinterpret_cast<const f32x4*>(bni + co);
+      const f32x2 t0 = ks_pk_sub(a2[2 * q], f32x2{m[0], m[1]}) * f32x2{iv[0], iv[1]};
+      const f32x2 t1 = ks_pk_sub(a2[2 * q + 1], f32x2{m[2], m[3]}) * f32x2{iv[2], iv[3]};
       bf16x4 y;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) y[e] = (bf16_t)((acc[4 * q + e] - m[e]) * iv[e]);
+      y[0] = (bf16_t)t0[0]; y[1] = (bf16_t)t0[1];
+      y[2] = (bf16_t)t1[0]; y[3] = (bf16_t)t1[1];
       y = relu_bf16(y);
       const uint2 d = __builtin_bit_cast(uint2, y);
       yd[q][0] = d.x;
@@ -306,20 +354,34 @@ __global__ __launch_bounds__(KS_NT) void conv3x3_ks(ConvParams p) {
       if (HAS_Z) {
         const bf16x8 xb = *reinterpret_cast<const bf16x8*>(
             xzb + (32 * gown + r32) * (KS_C * 2) + (32 * cg + 16 * i + 8 * h) * 2);
-        const bf16x8 yb = __builtin_bit_cast(bf16x8, yc);
+        const u32x4 xw = __builtin_bit_cast(u32x4, xb);
         bf16x8 zb;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) zb[e] = (bf16_t)((float)xb[e] + (float)yb[e]);
+        for (int e = 0; e < 4; ++e) {
+          // bf16 pairs widened to fp32 pairs, one packed add: (float)x + (float)y
+          const f32x2 z2 = f32x2{__builtin_bit_cast(float, xw[e] << 16), __builtin_bit_cast(float, xw[e] & 0xFFFF0000u)} +
+                           f32x2{__builtin_bit_cast(float, yc[e] << 16), __builtin_bit_cast(float, yc[e] & 0xFFFF0000u)};
+          zb[2 * e] = (bf16_t)z2[0];
+          zb[2 * e + 1] = (bf16_t)z2[1];
+        }
         ks_st16(inpx ? (void*)(Z + pix * p.ldy2 + 32 * cg + 16 * i + 8 * h) : (void*)&g_ks_sink[ln],
                 __builtin_bit_cast(u32x4, zb));
       }
     }
+    stamp(tj, 6);
     // window tj+1 has landed: younger are only this tile's stores
+    // (a diagnostic stamp store above only makes this wait stricter)
     if (HAS_Z) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     __syncthreads();   // D: next window visible; partials read before they are rewritten
+    stamp(tj, 7);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+hipError_t ks_trace_read(void* dst, size_t bytes) {
+  if (bytes > sizeof(g_ks_trace)) bytes = sizeof(g_ks_trace);
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_ks_trace), bytes, 0, hipMemcpyDeviceToHost);
 }
 
 int conv3_ks_ok(const ConvParams& p) {

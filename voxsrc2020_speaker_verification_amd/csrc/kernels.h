@@ -91,6 +91,7 @@ hipError_t launch_chain_rows(const ChainParams& q, hipStream_t s);
 int chain_fused_lds(int cin, int wid, int split, int W);
 // diagnostics: bneck_fused's per-step clock stamps of block 0 (VOXEMB_BNECK_DBG & 256)
 hipError_t bneck_trace_read(void* dst, size_t bytes);
+hipError_t ks_trace_read(void* dst, size_t bytes);   // conv3x3_ks stamps (diagnostic build)
 hipError_t launch_chain_fused(const ChainParams& q, hipStream_t s);
 // Stride-2 split (bneck.hip): branches k < split-1 (3x3 s2 + BN + ReLU) and the
 // last split's 3x3/2 average pool, q.R output rows per segment, q.nwaves
