@@ -29,7 +29,7 @@ class GconvParams(C.Structure):
                 ("N", C.c_int), ("H", C.c_int), ("W", C.c_int), ("C", C.c_int),
                 ("Ho", C.c_int), ("Wo", C.c_int), ("gw", C.c_int),
                 ("sh", C.c_int), ("ph", C.c_int), ("pw", C.c_int),
-                ("seg", C.c_int), ("nseg", C.c_int)]
+                ("seg", C.c_int), ("nseg", C.c_int), ("rs_force", C.c_int)]
 
 
 def tf_same(n, s, k=3):

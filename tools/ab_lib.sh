@@ -14,7 +14,7 @@ if [ -n "$TESTS" ]; then
   tail -1 gpurun_out/${TAG}_tests.log
 fi
 run() { local name=$1 lib=$2
-  VOXEMB_LIB=$lib timeout -k 10 200 python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --dump-ops \
+  VOXEMB_LIB=$lib timeout -k 10 200 python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --dump-ops ${BENCH_ARGS} \
     > gpurun_out/${TAG}_$name.json 2> gpurun_out/${TAG}_${name}_ops.txt || { echo "$name rc=$?"; exit 1; }
   python3 -c "import json; d=json.load(open('gpurun_out/${TAG}_$name.json')); print('$name', d['value'], d['ms_per_step'])"; }
 run old0 $P/libvoxemb_old.so && run new0 $P/libvoxemb.so && run old1 $P/libvoxemb_old.so && run new1 $P/libvoxemb.so

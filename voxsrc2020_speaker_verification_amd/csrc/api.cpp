@@ -284,6 +284,10 @@ struct vox_model {
   int no_conv3_utt = 0;    // VOXEMB_NO_CONV3_UTT: conv3x3_pipe for the w = 192 stride-1 branches
   int no_conv3_s2r = 0;    // VOXEMB_NO_CONV3_S2R: conv3x3_pipe for the w = 96 stride-2 branches
   int no_gconv = 0;        // VOXEMB_NO_GCONV: grouped 3x3 on the generic implicit GEMM
+  int gconv_rs = 0;        // VOXEMB_GCONV_RS: grouped 3x3 output rows per step (0 = default)
+  int gconv_wgs = 1024;    // VOXEMB_GCONV_WGS: grouped 3x3 workgroups the row segments aim for
+                           // (1,024: 2 segments per utterance at stage 3, 1,453 -> 1,424 us
+                           // over its 11 launches against 2,048)
   int no_conv3 = 0;        // VOXEMB_NO_CONV3: every 3x3 branch kernel off
   int no_gemm_pro = 0;     // VOXEMB_NO_GEMM_PRO: prologue 1x1 convs off the LDS-DMA GEMMs
   int no_gemm_taps = 0;    // VOXEMB_NO_GEMM_TAPS: TDNN dilated convs off gemm1x1_ws
@@ -332,6 +336,8 @@ static const PlanEnv kPlanEnv[] = {
     {"VOXEMB_NO_CONV3_UTT", &vox_model::no_conv3_utt},
     {"VOXEMB_NO_CONV3_S2R", &vox_model::no_conv3_s2r},
     {"VOXEMB_NO_GCONV", &vox_model::no_gconv},
+    {"VOXEMB_GCONV_RS", &vox_model::gconv_rs},
+    {"VOXEMB_GCONV_WGS", &vox_model::gconv_wgs},
     {"VOXEMB_NO_CONV3", &vox_model::no_conv3},
     {"VOXEMB_NO_GEMM_PRO", &vox_model::no_gemm_pro},
     {"VOXEMB_NO_GEMM_TAPS", &vox_model::no_gemm_taps},
@@ -1588,12 +1594,13 @@ static int build_dpn(Builder& B, const float* x, int n, int t, float* out) {
           g.w = c2.wgc ? c2.wgc->p : nullptr; g.y = Bb; g.ldy = r;
           g.N = n; g.H = Hi; g.W = Wi; g.C = r; g.Ho = Ho; g.Wo = Wo; g.gw = c2.cin;
           g.sh = bs; g.ph = tf_same_beg(Hi, 3, bs); g.pw = tf_same_beg(Wi, 3, bs);
+          g.rs_force = m->gconv_rs;
           if (c2.wgc && !m->no_gconv && c2.cin * c2.groups == r && gconv_ok(g)) {
             // row segments: enough workgroups to cover the chip a few times over,
             // each segment >= 4 steps (warm-up window re-read per segment)
             const int rs = gconv_rs(g);
             int nseg = 1;
-            while ((long)n * (r / 64) * nseg < 2048 && Ho / (2 * nseg) >= 4 * rs) nseg *= 2;
+            while ((long)n * (r / 64) * nseg < m->gconv_wgs && Ho / (2 * nseg) >= 4 * rs) nseg *= 2;
             g.seg = (Ho + nseg - 1) / nseg;
             g.nseg = (Ho + g.seg - 1) / g.seg;
             Op op;

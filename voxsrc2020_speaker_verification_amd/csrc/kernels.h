@@ -206,6 +206,7 @@ struct GconvParams {
   int N, H, W, C, Ho, Wo, gw;
   int sh, ph, pw;
   int seg, nseg;
+  int rs_force;   // output rows per step (0 = gconv_rs's choice; plan switch VOXEMB_GCONV_RS)
 };
 int gconv_ok(const GconvParams& p);
 int gconv_rs(const GconvParams& p);
