@@ -60,6 +60,20 @@ __device__ __forceinline__ void gw_glds16(const void* src, uint32_t lds) {
       : "memory");
 }
 
+// (diagnostics) the same with the non-temporal policy
+__device__ __forceinline__ void gw_glds16_nt(const void* src, uint32_t lds) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off nt\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(lds)
+      : "memory");
+}
+
 // the trailing s_nop keeps the next instruction from overwriting the data
 // registers before the store has read them
 __device__ __forceinline__ void gw_st16(void* dst, u32x4 v) {
@@ -383,7 +397,9 @@ constexpr int GS_NL = 4;   // loader waves
 // DBG (diagnostics, VOXEMB_GEMM_VAR 21/22): 1 = compute waves skip fragment
 // reads and MFMAs (stores kept), 2 = loaders issue no DMA, 8 = loaders skip
 // the weight pieces (operand + residual DMA only), 64 = no output stores,
-// 128 = loaders skip the residual pieces; results garbage
+// 128 = loaders skip the residual pieces; results garbage.  Same results, other
+// policies: 256 / 512 = nt / sc1 output stores, 1024 / 2048 = nt residual /
+// activation DMA (VOXEMB_GEMM_VAR 33 / 34 / 35 / 36)
 // MODE (operand variants; 0 = the Res2Net 1x1s):
 //   GS_PRO : BN + ReLU prologue on the B operand, relu((x - m[k]) * inv[k])
 //            rounded to bf16, as gemm1x1_pipe<.., PRO> (DPN bn_relu_conv,
@@ -547,7 +563,9 @@ __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
               const int hi = tho[i] + sh_t;
               a = (hi >= 0 && hi < p.H) ? src[i] + (size_t)hi * p.ldx + ci0 : zero;
             }
-            if (!(DBG & 2) && !((DBG & 8) && i < BN / 64))
+            if ((DBG & 2048) && i >= BN / 64)   // (diagnostics: activation pieces nt)
+              gw_glds16_nt(a, lds0 + (uint32_t)slot * SLOTB + (uint32_t)(u * SUBB) + (uint32_t)gi * 1024u);
+            else if (!(DBG & 2) && !((DBG & 8) && i < BN / 64))
               gw_glds16(a, lds0 + (uint32_t)slot * SLOTB + (uint32_t)(u * SUBB) + (uint32_t)gi * 1024u);
           }
         }
@@ -561,7 +579,10 @@ __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
           const int row = 2 * gi + (lane >> 5);
           const int c = (lane & 31) ^ (row & 15);
           const int pix = min(l_px0 + (BM / 4) * (gi >> 3) + 16 * ph + (row & 15), M - 1);
-          if (!(DBG & 2) && !(DBG & 128))
+          if (DBG & 1024)   // (diagnostics: residual pieces nt)
+            gw_glds16_nt(R + (size_t)pix * p.ldr + l_co0 + c * 8,
+                         lds0 + (uint32_t)slot * SLOTB + (uint32_t)gi * 1024u);
+          else if (!(DBG & 2) && !(DBG & 128))
             gw_glds16(R + (size_t)pix * p.ldr + l_co0 + c * 8,
                       lds0 + (uint32_t)slot * SLOTB + (uint32_t)gi * 1024u);
         }
@@ -895,7 +916,7 @@ hipError_t launch_gemm_wide(const ConvParams& p0, int num_cu, int variant, hipSt
   // VOXEMB_GEMM_VAR=-1 selects gemm1x1_wide
   if (variant == 0) variant = 1;
   if (variant == -1) variant = 0;
-  if (variant == 1 || (variant >= 21 && variant <= 34)) {   // wave-specialised
+  if (variant == 1 || (variant >= 21 && variant <= 36)) {   // wave-specialised
     auto go = [&](auto dbgc) {
       constexpr int D = decltype(dbgc)::value;
       const size_t lds64 = 2 * 2 * (size_t)(bn + bm) * 64 + 8 * (size_t)p.coutp;
@@ -945,6 +966,8 @@ hipError_t launch_gemm_wide(const ConvParams& p0, int num_cu, int variant, hipSt
     else if (variant == 23) go(std::integral_constant<int, 128>{});
     else if (variant == 33) go(std::integral_constant<int, 256>{});
     else if (variant == 34) go(std::integral_constant<int, 512>{});
+    else if (variant == 35) go(std::integral_constant<int, 1024>{});
+    else if (variant == 36) go(std::integral_constant<int, 2048>{});
     else
 #endif
       go(std::integral_constant<int, 0>{});
