@@ -405,6 +405,25 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.model, F, T, blob)
+        # like for like: the CPU baseline computes in fp32, the headline in bf16;
+        # the same workload through the GPU's fp32 path, a few timed steps
+        if args.precision == "bf16":
+            ex32 = Extractor(blob, device=dev.index, precision="fp32")
+            out32 = torch.empty((B, ex32.dim), dtype=torch.float32, device=dev)
+            ex32.run_device(x, out32, stream)
+            torch.cuda.synchronize(dev)
+            n32, t32 = 3, time.perf_counter()
+            for _ in range(n32):
+                ex32.run_device(x, out32, stream)
+            torch.cuda.synchronize(dev)
+            v32 = B * n32 / (time.perf_counter() - t32)
+            ex32.close()
+            cpu["gpu_fp32_same_workload"] = {
+                "value": round(v32, 1), "unit": "utterances/sec", "steps": n32,
+                "ratio_to_cpu": round(v32 / cpu["value"], 2),
+                "note": "the timed workload through the GPU's fp32 path (the CPU baseline's "
+                        "precision); the bf16 line's ratio is ratio_bf16_to_cpu"}
+            cpu["ratio_bf16_to_cpu"] = round(value / cpu["value"], 2)
 
     if rank == 0:
         line = {

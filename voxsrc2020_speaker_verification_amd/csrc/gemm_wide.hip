@@ -420,9 +420,11 @@ __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
   static_assert(KSUB == 1 || (KSUB == 2 && !PRO), "two k-steps per slot: plain or taps operands");
   constexpr int SUBB = (BN + BM) * 64;                    // one k-step's operands
   constexpr int SLOTB = KSUB == 1 ? GW_SLOT : KSUB * SUBB;
-  // ring slots: 4 of 32 KB at one k-step per slot; at two, 3 slots where they fit
-  // (128-pixel tiles) and 2 otherwise (64-deep steps of the 448-row tiles, one in flight)
-  constexpr int NSTR = KSUB == 1 ? GW_NST : (3 * SLOTB <= 147456 ? 3 : 2);
+  // ring slots: 4 of 32 KB at one k-step per slot, 3 at two (the 128-pixel tiles;
+  // 64-deep steps on the 448-row tiles fit only 2 slots, one step in flight, and
+  // measured 2 % slower: DESIGN.md, Round 5)
+  constexpr int NSTR = KSUB == 1 ? GW_NST : 3;
+  static_assert(NSTR * SLOTB <= 147456, "ring slots");
   constexpr int NI = BN / 32;
   constexpr int NQ = NI / 2;
   constexpr int NJ = BM / 64;                // 16-pixel columns per wave
@@ -599,10 +601,9 @@ __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
     };
     set_load_tile(0);
     issue(0);
-    // pieces of the NSTR - 2 steps after the awaited one (n1 unused with 3 slots,
-    // neither with 2: the awaited step is the only one in flight)
+    // pieces of the NSTR - 2 steps after the awaited one (n1 unused with 3 slots)
     int n1 = NSTR == 4 ? issue(1) : 0;
-    int n2 = NSTR >= 3 ? issue(NSTR - 2) : 0;
+    int n2 = issue(NSTR - 2);
     // GS_PRO: this lane's K chunk within a k-step (the DMA swizzle of an
     // activation row depends only on the lane: row = 16 gi + lane / 4)
     const int pc = (lane & 3) ^ ((4 - ((lane >> 4) & 3)) & 3);
@@ -641,7 +642,7 @@ __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
       __builtin_amdgcn_sched_barrier(0);
       const int n3 = issue((s + NSTR - 1) % NSTR);
       n1 = NSTR == 4 ? n2 : 0;
-      n2 = NSTR >= 3 ? n3 : 0;
+      n2 = n3;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     return;
@@ -858,7 +859,7 @@ int gemm_wide_bm(const ConvParams& p0, int num_cu) {
 }
 
 hipError_t launch_gemm_wide(const ConvParams& p0, int num_cu, int variant, hipStream_t s, int ksub_on,
-                             int force_bm, int bk64) {
+                             int force_bm) {
   const int bn = gemm_wide_bn(p0);
   if (!bn) return hipErrorInvalidValue;
   ConvParams p = p0;
@@ -919,16 +920,7 @@ hipError_t launch_gemm_wide(const ConvParams& p0, int num_cu, int variant, hipSt
   if (variant == 1 || (variant >= 21 && variant <= 36)) {   // wave-specialised
     auto go = [&](auto dbgc) {
       constexpr int D = decltype(dbgc)::value;
-      const size_t lds64 = 2 * 2 * (size_t)(bn + bm) * 64 + 8 * (size_t)p.coutp;
-      if (bk64 && ksub_on && bm != 128 && (p.kp / 32) % 2 == 0 && bn <= 256) {
-        // (plan switch VOXEMB_GEMM_BK64) 64-deep steps, two slots
-        if (bn == 192)
-          hipLaunchKernelGGL((gemm1x1_ws<192, false, 256, 0, 0, 2>), dim3(Gb), dim3(GS_NT), lds64, s, p);
-        else if (p.flags & EPI_RES)
-          hipLaunchKernelGGL((gemm1x1_ws<256, true, 192, 0, 0, 2>), dim3(Gb), dim3(GS_NT), lds64, s, p);
-        else
-          hipLaunchKernelGGL((gemm1x1_ws<256, false, 192, 0, 0, 2>), dim3(Gb), dim3(GS_NT), lds64, s, p);
-      } else if (two && bn == 192) {
+      if (two && bn == 192) {
         hipLaunchKernelGGL((gemm1x1_ws<192, false, 128, 0, 0, 2>), dim3(Gb), dim3(GS_NT), lds2, s, p);
       } else if (two && (p.flags & EPI_RES)) {
         hipLaunchKernelGGL((gemm1x1_ws<256, true, 128, 0, 0, 2>), dim3(Gb), dim3(GS_NT), lds2, s, p);
