@@ -301,7 +301,6 @@ struct vox_model {
   int pro_min_cout = 192;  // VOXEMB_PRO_MIN_COUT: narrowest prologue 1x1 on gemm1x1_ws
   int gemm_ksub1 = 0;      // VOXEMB_GEMM_KSUB1: gemm1x1_ws's 128-pixel tiles with one k-step
                            // per ring slot instead of two (bitwise A/B)
-  int gemm_bm = 0;         // VOXEMB_GEMM_BM: 128 = gemm1x1_ws's 128-pixel tiles on every launch
   int gemm_var = 0;        // VOXEMB_GEMM_VAR: -1 = gemm1x1_wide instead of gemm1x1_ws
                            // (bitwise A/B); other values are diagnostics (VOX_DIAG builds)
   int gemm_min_k = 128;    // VOXEMB_GEMM_MIN_K: smallest K routed to the LDS GEMMs (the K = 128
@@ -350,7 +349,6 @@ static const PlanEnv kPlanEnv[] = {
     {"VOXEMB_PRO_MIN_COUT", &vox_model::pro_min_cout},
     {"VOXEMB_GEMM_VAR", &vox_model::gemm_var},
     {"VOXEMB_GEMM_KSUB1", &vox_model::gemm_ksub1},
-    {"VOXEMB_GEMM_BM", &vox_model::gemm_bm},
     {"VOXEMB_GEMM_MIN_K", &vox_model::gemm_min_k},
     {"VOXEMB_NO_CHAIN", &vox_model::no_chain},
     {"VOXEMB_NO_STEM", &vox_model::no_stem},
@@ -1751,7 +1749,7 @@ static hipError_t run_op(vox_model* m, const Op& op, hipStream_t s) {
     case 18: return launch_gemm_pipe(op.cp, m->num_cu, m->gemm_var, s);
     case 19: return launch_gconv(op.gq, s);
     case 20: return launch_conv3_pipe(op.cp, m->num_cu, s);
-    case 21: return launch_gemm_wide(op.cp, m->num_cu, m->gemm_var, s, !m->gemm_ksub1, m->gemm_bm);
+    case 21: return launch_gemm_wide(op.cp, m->num_cu, m->gemm_var, s, !m->gemm_ksub1);
     case 10: return launch_split_chain(op.ch, op.cl.wco, op.cl.wpx, s);
     case 12: return launch_bneck(op.bq, op.cin, op.C, op.cl.wco, op.S, s);
     case 13: return launch_chain_rows(op.ch, s);

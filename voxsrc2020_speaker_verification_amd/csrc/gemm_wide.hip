@@ -858,8 +858,7 @@ int gemm_wide_bm(const ConvParams& p0, int num_cu) {
   return bn == 320 ? 128 : ws_bm(p0.N * p0.Ho * p0.Wo, coutp / bn, bn, num_cu);
 }
 
-hipError_t launch_gemm_wide(const ConvParams& p0, int num_cu, int variant, hipStream_t s, int ksub_on,
-                             int force_bm) {
+hipError_t launch_gemm_wide(const ConvParams& p0, int num_cu, int variant, hipStream_t s, int ksub_on) {
   const int bn = gemm_wide_bn(p0);
   if (!bn) return hipErrorInvalidValue;
   ConvParams p = p0;
@@ -871,7 +870,7 @@ hipError_t launch_gemm_wide(const ConvParams& p0, int num_cu, int variant, hipSt
   G = G >= 8 ? G / 8 * 8 : G;   // small launches (any_m) keep their few tiles
   const size_t lds = GW_NST * GW_SLOT + 8 * (size_t)p.coutp + (p.in_mean ? 8 * (size_t)p.kp : 0);
   // (the 320-wide tile holds 80 accumulators per compute wave at 128 pixels)
-  const int bm = bn == 320 || (force_bm == 128 && !p.in_mean) ? 128 : ws_bm(M, p.coutp / bn, bn, num_cu);
+  const int bm = bn == 320 ? 128 : ws_bm(M, p.coutp / bn, bn, num_cu);
   auto grid_for = [&](int bmx) {
     const int t = ((M + bmx - 1) / bmx) * (p.coutp / bn);
     int g = num_cu < t ? num_cu : t;

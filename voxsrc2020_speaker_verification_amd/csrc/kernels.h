@@ -170,8 +170,7 @@ int gemm_wide_bn(const ConvParams& p);
 int gemm_wide_bm(const ConvParams& p, int num_cu);
 // ksub_on: gemm1x1_ws's 128-pixel tiles take two 32-deep k-steps per ring slot
 // and barrier where they fit (bitwise the same outputs)
-hipError_t launch_gemm_wide(const ConvParams& p, int num_cu, int variant, hipStream_t s, int ksub_on = 1,
-                             int force_bm = 0);
+hipError_t launch_gemm_wide(const ConvParams& p, int num_cu, int variant, hipStream_t s, int ksub_on = 1);
 // Persistent LDS-DMA pipelined 3x3 implicit GEMM (conv3.hip) for the Res2Net
 // branch convs with Cin in {96, 192}: stride 1 (SAME) or 2 (fixed pad 1),
 // Cout % 96 == 0, epilogue BN + ReLU; with y2 set (stride 1) it also writes
