@@ -39,7 +39,17 @@ for w in range(8):
     b1 = (t[w, :, 2] - t[w, :, 1]).mean()
     p1 = (t[w, :, 3] - t[w, :, 2]).mean()
     b2 = (t[w, 1:, 0] - t[w, :-1, 3]).mean()
-    if int(os.environ.get("VOXEMB_BNECK_DBG", "0")) & 1024:
+    if int(os.environ.get("VOXEMB_BNECK_DBG", "0")) & 2048:
+        # stamp 1 exists only on the 1x1c waves' steps that own an output row
+        ok = t[w, :, 1] > t[w, :, 0]
+        if ok.any():
+            p0 = (t[w, ok, 1] - t[w, ok, 0]).mean()
+            b1 = (t[w, ok, 2] - t[w, ok, 1]).mean()
+        else:
+            p0, b1 = 0.0, (t[w, :, 2] - t[w, :, 0]).mean()
+        print(f"wave {w}: residual wait {p0:7.0f}  phase-0 work {b1:7.0f}  res issue+barrier1 {p1:7.0f}  "
+              f"phase 1 + barrier 2 {b2:7.0f}  ({int(ok.sum())} owning steps)")
+    elif int(os.environ.get("VOXEMB_BNECK_DBG", "0")) & 1024:
         print(f"wave {w}: phase0 {p0:7.0f}  barrier1+staging {b1:7.0f}  chain MFMA loop {p1:7.0f}  "
               f"epilogue+barrier2 {b2:7.0f}")
     else:

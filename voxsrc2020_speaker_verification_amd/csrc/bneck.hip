@@ -359,6 +359,7 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
       vm_wait(t < 1 ? 0 : K::IREG + 4 * nst);
 #pragma unroll
       for (int j = 0; j < PT; ++j) vm_launder(res[j]);
+      if (VOX_DBG(q) & 2048) stamp(t, 1);   // (residual row landed)
       // B chunk s of lane group g: concat channel 32s+8g -> (plane, offset)
       const char* src[K::KSC];
 #pragma unroll
@@ -443,12 +444,16 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
 #pragma unroll
       for (int j = 0; j < PT; ++j) vm_launder(res[j]);
     }
+    // (VOXEMB_BNECK_DBG bit 2048: stamps 1, 2, 3 after the 1x1c's residual wait,
+    // after the phase-0 work and after barrier 1, to split phase 0)
+    if (VOX_DBG(q) & 2048) stamp(t, 2);
     if (!(VOX_DBG(q) & 8)) load_res_at(rnext);
-    stamp(t, 1);
+    if (!(VOX_DBG(q) & 2048)) stamp(t, 1);
     __syncthreads();
+    if (VOX_DBG(q) & 2048) stamp(t, 3);
     // (VOXEMB_BNECK_DBG bit 1024: stamps 2 and 3 after the input staging and
     // after the chain's MFMA loop instead, to split phase 1)
-    if (!(VOX_DBG(q) & 1024)) stamp(t, 2);
+    if (!(VOX_DBG(q) & 1024) && !(VOX_DBG(q) & 2048)) stamp(t, 2);
     // ---------------- phase 1: all 3x3 stages, stage k on row a-2k+1
     if (!(VOX_DBG(q) & 8)) {
       // input row a+1 (loaded at step t-2): younger are step t-1's and this
@@ -535,7 +540,7 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
     } else if (VOX_DBG(q) & 1024) {
       stamp(t, 3);
     }
-    if (!(VOX_DBG(q) & 1024)) stamp(t, 3);
+    if (!(VOX_DBG(q) & 1024) && !(VOX_DBG(q) & 2048)) stamp(t, 3);
     __syncthreads();
   };
   for (int t = 0; t < steps; t += 2) {
