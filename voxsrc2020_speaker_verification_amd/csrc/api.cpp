@@ -1032,6 +1032,28 @@ static void emit_stem(Builder& B, const ConvW& stem, const float* x, int n, int 
   emit_conv(B, stem, in, nullptr, 0, 1, 1, 1, 1, 1, 1, H, W, y, stem.cout, EPI_AFFINE | EPI_RELU);
 }
 
+// Row segments per utterance for a row-streamed kernel that runs one workgroup
+// per CU (LDS-bound): the count that minimises (workgroup rounds) x (segment
+// rows + warm-up rows a segment recomputes), segments of >= min_rows rows.  At
+// B = 256 every utterance is one segment (one round); at B = 192 the L1
+// bottleneck takes 4 segments (3 rounds of 59 rows) where doubling until the
+// grid covers the chip took 2 (2 rounds of 109).
+static int row_segments(int n, int rows, int warm, int min_rows, int num_cu) {
+  int nseg = 1;
+  long best = -1;
+  for (int ns = 1; ns <= 16; ++ns) {
+    const int sg = (rows + ns - 1) / ns;
+    if (ns > 1 && sg < min_rows) break;
+    const long wgs = (long)n * ((rows + sg - 1) / sg);
+    const long cost = (wgs + num_cu - 1) / num_cu * (sg + warm);
+    if (best < 0 || cost < best) {
+      best = cost;
+      nseg = ns;
+    }
+  }
+  return nseg;
+}
+
 static int build_tdnn(Builder& B, const float* x, int n, int t, float* out) {
   vox_model* m = B.m;
   const int F = m->feat_dim;
@@ -1099,10 +1121,8 @@ static int build_res2net(Builder& B, const float* x, int n, int t, float* out) {
           BneckParams q{};
           void* yo = B.base(nxt_s, (size_t)n * H * W * C * es);
           q.x = cur.p; q.y = yo; q.N = n; q.H = H; q.W = W;
-          // one workgroup per CU: split utterances into row segments until the
-          // grid covers the chip (segments keep >= 16 rows; 3(s-1) warm-up rows each)
-          int nseg = 1;
-          while (n * nseg < 256 && H / (2 * nseg) >= 16) nseg *= 2;
+          // one workgroup per CU (3(s-1) warm-up rows per segment)
+          int nseg = row_segments(n, H, 3 * (s - 1), 16, m->num_cu);
           if (m->bneck_nseg > 0) nseg = std::min(m->bneck_nseg, H);
           q.seg = (H + nseg - 1) / nseg;
           q.nseg = (H + q.seg - 1) / q.seg;
@@ -1160,8 +1180,8 @@ static int build_res2net(Builder& B, const float* x, int n, int t, float* out) {
           q.wa = c1a.wpair->p; q.ma = (const float*)c1a.mean->p; q.ia = (const float*)c1a.inv->p;
           q.b = Bc; q.ldb = sw;
           q.N = n; q.H = H; q.W = W; q.w = w; q.nst = s - 1;
-          int nseg = 1;
-          while (n * nseg < 256 && Ho / (2 * nseg) >= 8) nseg *= 2;
+          // (one workgroup per CU; one warm-up step per segment)
+          int nseg = row_segments(n, Ho, 1, 8, m->num_cu);
           q.R = (Ho + nseg - 1) / nseg;
           q.nwaves = (Ho + q.R - 1) / q.R;
           for (int j = 0; j < s - 1; ++j) {
@@ -1198,8 +1218,8 @@ static int build_res2net(Builder& B, const float* x, int n, int t, float* out) {
           q.wa = c1a.wpair->p; q.ma = (const float*)c1a.mean->p; q.ia = (const float*)c1a.inv->p;
           q.b = Bc; q.ldb = sw;
           q.N = n; q.H = H; q.W = W; q.w = w; q.nst = s - 1;
-          int nseg = 1;
-          while (n * nseg < 256 && H / (2 * nseg) >= 16) nseg *= 2;
+          // (one workgroup per CU; the stage lags recompute 2(s-1) rows per segment)
+          int nseg = row_segments(n, H, 2 * (s - 1), 16, m->num_cu);
           q.R = (H + nseg - 1) / nseg;
           q.nwaves = (H + q.R - 1) / q.R;
           for (int j = 0; j < s - 1; ++j) {
@@ -1242,8 +1262,8 @@ static int build_res2net(Builder& B, const float* x, int n, int t, float* out) {
           ChainParams q{};
           q.a = A; q.lda = sw; q.b = Bc; q.ldb = sw;
           q.N = n; q.H = H; q.W = W; q.w = w; q.nst = s - 1;
-          int nseg = 1;
-          while (n * nseg < 256 && H / (2 * nseg) >= 16) nseg *= 2;
+          // (one workgroup per CU; the stage lags recompute 2(s-1) rows per segment)
+          int nseg = row_segments(n, H, 2 * (s - 1), 16, m->num_cu);
           q.R = (H + nseg - 1) / nseg;           // rows per segment
           q.nwaves = (H + q.R - 1) / q.R;        // segments per utterance
           double fl = 0;
@@ -1327,8 +1347,8 @@ static int build_res2net(Builder& B, const float* x, int n, int t, float* out) {
           ChainParams q{};
           q.a = A; q.lda = sw; q.b = Bc; q.ldb = sw;
           q.N = n; q.H = H; q.W = W; q.w = w; q.nst = s - 1;
-          int nseg = 1;
-          while (n * nseg < 256 && Ho / (2 * nseg) >= 8) nseg *= 2;
+          // (one workgroup per CU; one warm-up step per segment)
+          int nseg = row_segments(n, Ho, 1, 8, m->num_cu);
           q.R = (Ho + nseg - 1) / nseg;
           q.nwaves = (Ho + q.R - 1) / q.R;
           for (int j = 0; j < s - 1; ++j) {
