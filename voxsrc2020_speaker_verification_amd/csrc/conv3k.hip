@@ -23,11 +23,12 @@
 // (half 0) + (half 1) in fp32 -- one fixed order, whatever wave finishes it.
 //
 // Window layout: pixel-major, 13 16-B units per pixel slot (12 chunks of 8
-// channels + 1 pad unit).  The odd 208-B pitch puts the 16 lanes of every
-// ds_read_b128 lane group (16 distinct consecutive slots of one chunk) on 16
+// channels + 1 pad unit).  The odd 208-B pitch gives 16 consecutive slots 16
 // disjoint 4-bank sets, and a window DMA piece reads 192 contiguous bytes per
 // pixel.  One zero slot between window rows serves as both rows' SAME padding
-// column (SW = W + 1).  Tiles are utterance-aligned (the padding is per
+// column (SW = W + 1); its row breaks would put two lanes of a ds_read_b128
+// lane group on one bank set, so lanes take their group's pixels in a
+// permuted order (g_ks_perm).  Tiles are utterance-aligned (the padding is per
 // utterance); the window is double-buffered so the next tile's rows stream in
 // under this tile's MFMAs, and the y staging + deferred row-contiguous store
 // pass are conv3x3_rw's.
@@ -53,6 +54,9 @@ constexpr int KS_NCH = KS_C / 8;       // 12 chunks per pixel
 constexpr int KS_PU = KS_NCH + 1;      // units per window slot (odd: conflict-free reads)
 constexpr int KS_PB = KS_PU * 16;      // 208 B
 constexpr int KS_XCH = KS_NW * 4096;   // partial-sum exchange: 4 KB per wave
+#ifndef KS_PD
+#define KS_PD 2                        // B fragments read ahead of their MFMA
+#endif
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -91,6 +95,28 @@ __device__ uint4 g_ks_zero[4] = {};
 // the z-forming launches, [wave][tile < 16][stamp < 8] (tools/ks_trace.py)
 __device__ unsigned long long g_ks_trace[KS_NW * 16 * 8];
 __device__ uint4 g_ks_sink[64];   // destination of masked lanes' stores
+// lane -> pixel of a 32-pixel group, [W = 20, 10][(first pixel % W) / (W / 5)][lane]
+// (tools/ks_lane_perm.py): each pixel on the ds_read_b128 lane group that still lacks
+// its 4-bank quad; the window's row breaks put two lanes of a group on one quad when
+// pixel i sits on lane i (8 LDS cycles per fragment read instead of 5.6 for W = 20).
+// The MFMA column of a lane is its output pixel in the B operand and the accumulator
+// alike, so the permutation changes no arithmetic.
+__device__ const unsigned char g_ks_perm[2][5][32] = {
+    {  // W = 20
+        {0, 5, 10, 15, 16, 20, 25, 30, 24, 29, 19, 23, 9, 14, 3, 8, 28, 18, 22, 27, 13, 2, 7, 12, 1, 6, 11, 31, 17, 21, 26, 4},
+        {12, 1, 6, 11, 27, 16, 21, 26, 31, 20, 25, 30, 0, 5, 10, 15, 19, 24, 29, 18, 4, 9, 14, 3, 8, 13, 2, 7, 23, 28, 17, 22},
+        {0, 8, 12, 2, 15, 23, 28, 17, 22, 16, 21, 26, 7, 1, 6, 11, 20, 25, 30, 19, 5, 10, 14, 4, 9, 13, 3, 31, 24, 29, 18, 27},
+        {1, 0, 4, 8, 16, 15, 19, 24, 28, 18, 17, 22, 13, 3, 2, 7, 27, 21, 26, 20, 11, 6, 10, 5, 9, 14, 31, 30, 25, 29, 23, 12},
+        {0, 1, 4, 9, 15, 16, 20, 24, 29, 28, 18, 23, 14, 13, 3, 7, 27, 17, 22, 26, 12, 2, 6, 11, 5, 10, 30, 31, 21, 25, 19, 8},
+    },
+    {  // W = 10
+        {2, 1, 0, 14, 17, 16, 15, 29, 19, 23, 28, 18, 4, 9, 13, 3, 22, 27, 21, 26, 8, 12, 7, 11, 6, 10, 31, 30, 20, 25, 5, 24},
+        {2, 1, 0, 12, 17, 16, 15, 27, 21, 26, 20, 25, 7, 11, 6, 10, 19, 24, 28, 18, 5, 9, 14, 4, 8, 31, 30, 29, 23, 13, 3, 22},
+        {0, 2, 1, 10, 15, 16, 30, 25, 19, 24, 28, 18, 5, 9, 14, 4, 23, 27, 17, 22, 8, 13, 3, 7, 12, 6, 29, 31, 26, 21, 11, 20},
+        {2, 1, 0, 8, 16, 15, 14, 23, 27, 17, 22, 26, 13, 3, 7, 12, 21, 25, 20, 24, 6, 11, 5, 10, 4, 31, 30, 29, 19, 9, 28, 18},
+        {1, 0, 16, 6, 15, 14, 31, 21, 25, 20, 24, 19, 11, 5, 10, 4, 23, 28, 18, 22, 9, 13, 3, 8, 12, 2, 30, 29, 27, 17, 7, 26},
+    },
+};
 
 template <int W>
 struct KsCfg {
@@ -208,6 +234,18 @@ __global__ __launch_bounds__(KS_NT) void conv3x3_ks(ConvParams p) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
+  // this lane's pixel offset in a group of each of the five bank patterns, 5 bits each
+  unsigned lperm = 0;
+#pragma unroll
+  for (int q = 0; q < 5; ++q) lperm |= (unsigned)g_ks_perm[W == 20 ? 0 : 1][q][r32] << (5 * q);
+  // consumed here, so the compiler's wait for these loads sits before the tile loop
+  // (inside it, its vmcnt would also count the hand-counted window DMA)
+  asm volatile("" : "+v"(lperm));
+  auto lpx = [&](int p0, int j) __attribute__((always_inline)) {
+    const int pat = ((p0 + 32 * j) % W) / (W / 5);
+    return (int)((lperm >> (5 * pat)) & 31u);
+  };
+
   // this wave finishes pixel group 2 ph + kh of every tile and hands its
   // partial of group 2 ph + (1 - kh) to its partner (cg, 1 - kh, ph)
   const int gown = 2 * ph + kh, gpart = 2 * ph + (1 - kh);
@@ -250,21 +288,22 @@ __global__ __launch_bounds__(KS_NT) void conv3x3_ks(ConvParams p) {
     // live across the loop they cost the weights' registers (spills)
     int ln = lane;
     asm volatile("" : "+v"(ln));
-    const int r32 = ln & 31, h = ln >> 5;
+    const int h = ln >> 5;
     // this lane's output pixel (group gown) and its 16-B cout chunks 16 i + 8 h
-    const int pxo = p0 + 32 * gown + r32;
+    const int ro = lpx(p0, gown);
+    const int pxo = p0 + 32 * gown + ro;
     const bool inpx = pxo < HW;
     const size_t pix = (size_t)n * HW + (inpx ? pxo : HW - 1);
     // byte address of the lane's pixel slot of group j shifted by (-1 row,
     // -1 column), chunk h; + a compile-time tap/chunk offset per k16-step
     auto base_of = [&](int j) __attribute__((always_inline)) {
-      const int pc = min(p0 + 32 * j + r32, HW - 1);
+      const int pc = min(p0 + 32 * j + lpx(p0, j), HW - 1);
       const int rr = pc / W - (p0 / W - 1);   // window row of the pixel (>= 1)
       return b * K::WBUF + KS_PB * ((rr - 1) * SW + (pc % W)) + 16 * h;
     };
     // one pass: the 27 k16-steps of K half KH over pixel group j, one
     // accumulation chain (32x32x16 needs no interleaving for throughput),
-    // fragments read two steps ahead
+    // fragments read KS_PD steps ahead (2; 3 and 4 measured the same)
     auto kpass = [&](auto khc, int j, auto&& fl) __attribute__((always_inline)) {
       constexpr int KH = decltype(khc)::value;
       auto off = [](int s) constexpr {
@@ -275,16 +314,17 @@ __global__ __launch_bounds__(KS_NT) void conv3x3_ks(ConvParams p) {
       f32x16 acc;
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[e] = 0.f;
-      bf16x8 bf[3];
-      bf[0] = *reinterpret_cast<const bf16x8*>(smem + bs + off(0));
-      bf[1] = *reinterpret_cast<const bf16x8*>(smem + bs + off(1));
+      bf16x8 bf[KS_PD + 1];
+#pragma unroll
+      for (int s = 0; s < KS_PD; ++s) bf[s] = *reinterpret_cast<const bf16x8*>(smem + bs + off(s));
 #pragma unroll
       for (int s = 0; s < KS_SH; ++s) {
         // hard scheduling fences: with sched_group_barrier hints alone the
         // compiler issued each read right before its MFMA (lgkmcnt(0) per MFMA)
-        if (s + 2 < KS_SH) bf[(s + 2) % 3] = *reinterpret_cast<const bf16x8*>(smem + bs + off(s + 2));
+        if (s + KS_PD < KS_SH)
+          bf[(s + KS_PD) % (KS_PD + 1)] = *reinterpret_cast<const bf16x8*>(smem + bs + off(s + KS_PD));
         __builtin_amdgcn_sched_barrier(0);
-        acc = mfma32(wr[s], bf[s % 3], acc);
+        acc = mfma32(wr[s], bf[s % (KS_PD + 1)], acc);
         fl(s);
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -353,7 +393,7 @@ __global__ __launch_bounds__(KS_NT) void conv3x3_ks(ConvParams p) {
       ks_st16(inpx ? (void*)(Y + off) : (void*)&g_ks_sink[ln], yc);
       if (HAS_Z) {
         const bf16x8 xb = *reinterpret_cast<const bf16x8*>(
-            xzb + (32 * gown + r32) * (KS_C * 2) + (32 * cg + 16 * i + 8 * h) * 2);
+            xzb + (32 * gown + ro) * (KS_C * 2) + (32 * cg + 16 * i + 8 * h) * 2);
         const u32x4 xw = __builtin_bit_cast(u32x4, xb);
         bf16x8 zb;
 #pragma unroll
