@@ -68,6 +68,13 @@ __device__ __forceinline__ f32x2 ks_pk_sub(f32x2 a, f32x2 b) {
   return r;
 }
 
+// two floats to a bf16 pair (round to nearest even, as a scalar conversion)
+__device__ __forceinline__ unsigned ks_cvt_pk(f32x2 v) {
+  unsigned r;
+  asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(v[0]), "v"(v[1]));
+  return r;
+}
+
 __device__ __forceinline__ void ks_glds16(const void* src, uint32_t lds) {
   unsigned keep;
   asm volatile(
@@ -371,9 +378,9 @@ __global__ __launch_bounds__(KS_NT) void conv3x3_ks(ConvParams p) {
       const f32x4 iv = *reinterpret_cast<const f32x4*>(bni + co);
       const f32x2 t0 = ks_pk_sub(a2[2 * q], f32x2{m[0], m[1]}) * f32x2{iv[0], iv[1]};
       const f32x2 t1 = ks_pk_sub(a2[2 * q + 1], f32x2{m[2], m[3]}) * f32x2{iv[2], iv[3]};
-      bf16x4 y;
-      y[0] = (bf16_t)t0[0]; y[1] = (bf16_t)t0[1];
-      y[2] = (bf16_t)t1[0]; y[3] = (bf16_t)t1[1];
+      // one v_cvt_pk_bf16_f32 per pair (element-wise the compiler converted each
+      // value alone and merged the halves with v_perm_b32: 16 extra per tile)
+      bf16x4 y = __builtin_bit_cast(bf16x4, uint2{ks_cvt_pk(t0), ks_cvt_pk(t1)});
       y = relu_bf16(y);
       const uint2 d = __builtin_bit_cast(uint2, y);
       yd[q][0] = d.x;
