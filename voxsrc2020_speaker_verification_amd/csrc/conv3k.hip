@@ -54,6 +54,9 @@ constexpr int KS_NCH = KS_C / 8;       // 12 chunks per pixel
 constexpr int KS_PU = KS_NCH + 1;      // units per window slot (odd: conflict-free reads)
 constexpr int KS_PB = KS_PU * 16;      // 208 B
 constexpr int KS_XCH = KS_NW * 4096;   // partial-sum exchange: 4 KB per wave
+#ifndef KS_STAGE
+#define KS_STAGE 1                     // y / z stores staged through LDS (0: from registers)
+#endif
 #ifndef KS_PD
 #define KS_PD 2                        // B fragments read ahead of their MFMA
 #endif
@@ -386,6 +389,45 @@ __global__ __launch_bounds__(KS_NT) void conv3x3_ks(ConvParams p) {
       yd[q][0] = d.x;
       yd[q][1] = d.y;
     }
+#if KS_STAGE
+    // y through the partner's partial-sum slot (this wave was its only reader):
+    // row r32 (pixel ro) x 32 couts, 64 B, 16-B chunks swizzled by (r32 >> 1) & 3
+    // (the b64 writes of 16 lanes then fall on 8 bank pairs, not 2); read back
+    // as 16 pixels x 64 B per instruction, so each y / z store touches 16 lines
+    // with 64 B instead of 32 with 32 B (stores ~17 % of the kernel, line-bound)
+    char* stg = smem + 2 * K::WBUF + partner * 4096;
+    {
+      const int r = ln & 31, sw = (r >> 1) & 3;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        *reinterpret_cast<uint2*>(stg + r * 64 + ((q ^ sw) * 16) + 8 * h) = uint2{yd[q][0], yd[q][1]};
+    }
+    asm volatile("" ::: "memory");   // same-wave LDS: in order in hardware; keep the compiler's order
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int r = (ln >> 2) + 16 * k, c = ln & 3;
+      const u32x4 yc = *reinterpret_cast<const u32x4*>(stg + r * 64 + ((c ^ ((r >> 1) & 3)) * 16));
+      const int rk = __builtin_amdgcn_ds_bpermute(4 * r, ro);   // pixel of row r (lane r's)
+      const int pk = p0 + 32 * gown + rk;
+      const bool ink = pk < HW;
+      const size_t pixk = (size_t)n * HW + (ink ? pk : HW - 1);
+      // always issued (a masked pixel stores to a sink line) so every wave's
+      // vmcnt count below is the same
+      ks_st16(ink ? (void*)(Y + pixk * p.ldy + 32 * cg + 8 * c) : (void*)&g_ks_sink[ln], yc);
+      if (HAS_Z) {
+        const u32x4 xw = *reinterpret_cast<const u32x4*>(xzb + (32 * gown + rk) * (KS_C * 2) + (32 * cg + 8 * c) * 2);
+        u32x4 zw;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          // bf16 pairs widened to fp32 pairs, one packed add: (float)x + (float)y
+          const f32x2 z2 = f32x2{__builtin_bit_cast(float, xw[e] << 16), __builtin_bit_cast(float, xw[e] & 0xFFFF0000u)} +
+                           f32x2{__builtin_bit_cast(float, yc[e] << 16), __builtin_bit_cast(float, yc[e] & 0xFFFF0000u)};
+          zw[e] = ks_cvt_pk(z2);
+        }
+        ks_st16(ink ? (void*)(Z + pixk * p.ldy2 + 32 * cg + 8 * c) : (void*)&g_ks_sink[ln], zw);
+      }
+    }
+#else
     // lanes l and l + 32 (same pixel) hold couts 8q..8q+3 and 8q+4..8q+7: one
     // half exchange per dword pair gives each lane 8 contiguous couts, chunk
     // i = 16 i + 8 h (T21 of the HIP guide)
@@ -415,6 +457,7 @@ __global__ __launch_bounds__(KS_NT) void conv3x3_ks(ConvParams p) {
                 __builtin_bit_cast(u32x4, zb));
       }
     }
+#endif
     stamp(tj, 6);
     // window tj+1 has landed: younger are only this tile's stores
     // (a diagnostic stamp store above only makes this wait stricter)
