@@ -28,6 +28,7 @@
 namespace vox {
 
 namespace {
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 constexpr int CU_C = 192;                // Cin = Cout = branch width
 constexpr int CU_NW = 12;
 constexpr int CU_NT = 64 * CU_NW;
@@ -232,19 +233,35 @@ __global__ __launch_bounds__(CU_NT) void conv3x3_utt(ConvParams p) {
       const f32x4 m = *reinterpret_cast<const f32x4*>(p.mean + co);
       const f32x4 iv = *reinterpret_cast<const f32x4*>(p.inv + co);
 #pragma unroll
-      for (int j = 0; j < CU_PG; ++j) {
-        const int px = 16 * (CU_PG * pg + j) + ecol;
-        if (px < npx) {
+      for (int jj = 0; jj < CU_PG / 2; ++jj) {
+        // pixel tiles 2 jj, 2 jj + 1: one half-row exchange per dword gives each
+        // lane 8 contiguous couts (g even: tile 2 jj, couts 16 i + 8 (g / 2);
+        // g odd: tile 2 jj + 1), so y and z go out as 16-B stores, half the
+        // store instructions of the 8-B ones (T21 with v_permlane16_swap)
+        unsigned d[2][2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
           bf16x4 o;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) o[e] = (bf16_t)fmaxf((acc[i][j][e] - m[e]) * iv[e], 0.f);
-          *reinterpret_cast<bf16x4*>(Y + (pbase + px) * p.ldy + co) = o;
+          for (int e = 0; e < 4; ++e) o[e] = (bf16_t)fmaxf((acc[i][2 * jj + t][e] - m[e]) * iv[e], 0.f);
+          const uint2 u = __builtin_bit_cast(uint2, o);
+          d[t][0] = u.x;
+          d[t][1] = u.y;
+        }
+        const auto s0 = __builtin_amdgcn_permlane16_swap(d[0][0], d[1][0], false, false);
+        const auto s1 = __builtin_amdgcn_permlane16_swap(d[0][1], d[1][1], false, false);
+        const u32x4 yc = {s0[0], s1[0], s0[1], s1[1]};
+        const int px = 16 * (CU_PG * pg + 2 * jj + (eg & 1)) + ecol;
+        const int cq = 48 * cg + 16 * i + 8 * (eg >> 1);
+        if (px < npx) {
+          *reinterpret_cast<u32x4*>(Y + (pbase + px) * p.ldy + cq) = yc;
           if (HAS_Z) {
-            const bf16x4 xv = *reinterpret_cast<const bf16x4*>(XZ + (pbase + px) * p.ldr + co);
-            bf16x4 zv;
+            const bf16x8 xv = *reinterpret_cast<const bf16x8*>(XZ + (pbase + px) * p.ldr + cq);
+            const bf16x8 ov = __builtin_bit_cast(bf16x8, yc);
+            bf16x8 zv;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) zv[e] = (bf16_t)((float)xv[e] + (float)o[e]);
-            *reinterpret_cast<bf16x4*>(Z + (pbase + px) * p.ldy2 + co) = zv;
+            for (int e = 0; e < 8; ++e) zv[e] = (bf16_t)((float)xv[e] + (float)ov[e]);
+            *reinterpret_cast<bf16x8*>(Z + (pbase + px) * p.ldy2 + cq) = zv;
           }
         }
       }
@@ -259,7 +276,7 @@ int conv3_utt_ok(const ConvParams& p) {
   if (p.Cin != CU_C || p.Cout != CU_C || p.kh != 3 || p.kw != 3 || p.groups != 1) return 0;
   if (p.sh != 1 || p.sw != 1 || p.dh != 1 || p.dw != 1 || p.ph != 1 || p.pw != 1) return 0;
   if (p.Ho != p.H || p.Wo != p.W || p.W != 10) return 0;
-  if (p.ldx % 8 || p.ldy % 4 || p.ldr % 4 || p.ldy2 % 4) return 0;
+  if (p.ldx % 8 || p.ldy % 8 || p.ldr % 8 || p.ldy2 % 8) return 0;   // 16-B epilogue stores
   if (p.flags != (EPI_AFFINE | EPI_RELU) || p.in_mean || p.x2 || !p.mean || !p.inv) return 0;
   if (p.y2 && p.y2 != p.res) return 0;   // z_{k+1} in place over x_{k+1}
   return p.N * p.H * p.W > 0;
