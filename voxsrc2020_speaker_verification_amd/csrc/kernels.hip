@@ -1188,82 +1188,95 @@ __global__ __launch_bounds__(256) void stem_conv1(const float* __restrict__ x, i
 // 80) -- and each wave's 64 output pixels are staged in LDS so that a store
 // instruction writes 1 KB contiguous (lane l: chunk l % 4 of pixel l / 4 + 16 s)
 // instead of 16 B at a 64-B lane stride (4x the L2 write requests: 111 -> 91
-// us); channel pairs on v_pk_fma_f32 and branch-free tap loads: 91 -> 80 us.
+// us); channel pairs on v_pk_fma_f32 and branch-free tap loads: 91 -> 78 us.
 // Same products, same tap order, same roundings: bitwise equal to stem_conv1.
+#ifndef STEM_PP
+#define STEM_PP 1   // pixels per thread (2: half the weight reads, measured 78 -> 84 us)
+#endif
 __global__ __launch_bounds__(256) void stem_conv1_c32(const float* __restrict__ x, int N, int H,
                                                      int W, const float* __restrict__ wts,
                                                      const float* __restrict__ mean,
                                                      const float* __restrict__ inv,
                                                      bf16_t* __restrict__ y) {
   typedef float f32x2 __attribute__((ext_vector_type(2)));
-  constexpr int COUT = 32;
+  constexpr int COUT = 32, PP = STEM_PP;   // PP pixels per thread, 256 apart
   __shared__ __attribute__((aligned(16))) float sw[9 * COUT];
   __shared__ __attribute__((aligned(16))) float sm[COUT], si[COUT];
-  __shared__ __attribute__((aligned(16))) uint4 st[256 * 4];
+  __shared__ __attribute__((aligned(16))) uint4 st[PP * 256 * 4];
   for (int i = threadIdx.x; i < 9 * COUT; i += blockDim.x) sw[i] = wts[i];
   for (int i = threadIdx.x; i < COUT; i += blockDim.x) { sm[i] = mean[i]; si[i] = inv[i]; }
   __syncthreads();
-  const int64_t pix0 = (int64_t)blockIdx.x * blockDim.x;
-  const int64_t pix = pix0 + threadIdx.x;
+  const int64_t pix0 = (int64_t)blockIdx.x * (PP * 256);
   const int64_t npix = (int64_t)N * H * W;
   const int lane = threadIdx.x & 63, wb = threadIdx.x & ~63;
-  if (pix < npix) {
+  // taps loaded unconditionally from clamped coordinates, then masked (the
+  // bounds-checked loads compiled to a branch per tap)
+  float v[PP][9];
+#pragma unroll
+  for (int u = 0; u < PP; ++u) {
+    const int64_t pix = min(pix0 + 256 * u + threadIdx.x, npix - 1);
     const unsigned hw = npix < ((int64_t)1 << 32) ? (unsigned)pix % (unsigned)(H * W)
                                                   : (unsigned)(pix % ((int64_t)H * W));
     const int hi = (int)(hw / (unsigned)W);
     const int wi = (int)(hw - (unsigned)hi * (unsigned)W);
-    // taps loaded unconditionally from clamped coordinates, then masked (the
-    // bounds-checked loads compiled to a branch per tap)
     const float* xi = x + (pix - (int64_t)hw);
-    float v[9];
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
       const int yy = hi + t / 3 - 1, xx = wi + t % 3 - 1;
       const bool ok = yy >= 0 && yy < H && xx >= 0 && xx < W;
       const int yc = min(max(yy, 0), H - 1), xc = min(max(xx, 0), W - 1);
       const float a = xi[yc * W + xc];
-      v[t] = ok ? (float)(bf16_t)a : 0.f;
+      v[u][t] = ok ? (float)(bf16_t)a : 0.f;
     }
+  }
 #pragma unroll
-    for (int c = 0; c < COUT / 8; ++c) {
-      const int c0 = 8 * c;
-      // channel pairs on v_pk_fma_f32 (each element the fmaf of the scalar
-      // chain, same tap order): the kernel was bound by VALU issue
-      f32x2 acc[4] = {};
+  for (int c = 0; c < COUT / 8; ++c) {
+    const int c0 = 8 * c;
+    // channel pairs on v_pk_fma_f32 (each element the fmaf of the scalar
+    // chain, same tap order): the kernel was bound by VALU issue
+    f32x2 acc[PP][4] = {};
 #pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const f32x4 w0 = *reinterpret_cast<const f32x4*>(sw + t * COUT + c0);
-        const f32x4 w1 = *reinterpret_cast<const f32x4*>(sw + t * COUT + c0 + 4);
-        const f32x2 vv = {v[t], v[t]};
-        acc[0] = __builtin_elementwise_fma(vv, f32x2{w0[0], w0[1]}, acc[0]);
-        acc[1] = __builtin_elementwise_fma(vv, f32x2{w0[2], w0[3]}, acc[1]);
-        acc[2] = __builtin_elementwise_fma(vv, f32x2{w1[0], w1[1]}, acc[2]);
-        acc[3] = __builtin_elementwise_fma(vv, f32x2{w1[2], w1[3]}, acc[3]);
+    for (int t = 0; t < 9; ++t) {
+      const f32x4 w0 = *reinterpret_cast<const f32x4*>(sw + t * COUT + c0);
+      const f32x4 w1 = *reinterpret_cast<const f32x4*>(sw + t * COUT + c0 + 4);
+#pragma unroll
+      for (int u = 0; u < PP; ++u) {
+        const f32x2 vv = {v[u][t], v[u][t]};
+        acc[u][0] = __builtin_elementwise_fma(vv, f32x2{w0[0], w0[1]}, acc[u][0]);
+        acc[u][1] = __builtin_elementwise_fma(vv, f32x2{w0[2], w0[3]}, acc[u][1]);
+        acc[u][2] = __builtin_elementwise_fma(vv, f32x2{w1[0], w1[1]}, acc[u][2]);
+        acc[u][3] = __builtin_elementwise_fma(vv, f32x2{w1[2], w1[3]}, acc[u][3]);
       }
-      const f32x4 m0 = *reinterpret_cast<const f32x4*>(sm + c0);
-      const f32x4 m1 = *reinterpret_cast<const f32x4*>(sm + c0 + 4);
-      const f32x4 i0 = *reinterpret_cast<const f32x4*>(si + c0);
-      const f32x4 i1 = *reinterpret_cast<const f32x4*>(si + c0 + 4);
-      const f32x2 t0 = (acc[0] - f32x2{m0[0], m0[1]}) * f32x2{i0[0], i0[1]};
-      const f32x2 t1 = (acc[1] - f32x2{m0[2], m0[3]}) * f32x2{i0[2], i0[3]};
-      const f32x2 t2 = (acc[2] - f32x2{m1[0], m1[1]}) * f32x2{i1[0], i1[1]};
-      const f32x2 t3 = (acc[3] - f32x2{m1[2], m1[3]}) * f32x2{i1[2], i1[3]};
+    }
+    const f32x4 m0 = *reinterpret_cast<const f32x4*>(sm + c0);
+    const f32x4 m1 = *reinterpret_cast<const f32x4*>(sm + c0 + 4);
+    const f32x4 i0 = *reinterpret_cast<const f32x4*>(si + c0);
+    const f32x4 i1 = *reinterpret_cast<const f32x4*>(si + c0 + 4);
+#pragma unroll
+    for (int u = 0; u < PP; ++u) {
+      const f32x2 t0 = (acc[u][0] - f32x2{m0[0], m0[1]}) * f32x2{i0[0], i0[1]};
+      const f32x2 t1 = (acc[u][1] - f32x2{m0[2], m0[3]}) * f32x2{i0[2], i0[3]};
+      const f32x2 t2 = (acc[u][2] - f32x2{m1[0], m1[1]}) * f32x2{i1[0], i1[1]};
+      const f32x2 t3 = (acc[u][3] - f32x2{m1[2], m1[3]}) * f32x2{i1[2], i1[3]};
       bf16x8 o;
       o[0] = (bf16_t)t0[0]; o[1] = (bf16_t)t0[1]; o[2] = (bf16_t)t1[0]; o[3] = (bf16_t)t1[1];
       o[4] = (bf16_t)t2[0]; o[5] = (bf16_t)t2[1]; o[6] = (bf16_t)t3[0]; o[7] = (bf16_t)t3[1];
       o = relu_bf16(o);   // == bf16(relu(x)) bit for bit (device_common.h)
       // chunk c of pixel lane at unit 4 lane + (c + lane / 2) % 4: conflict-free
       // 8-lane store groups and 16-lane read groups
-      st[4 * (wb + lane) + ((c + (lane >> 1)) & 3)] = __builtin_bit_cast(uint4, o);
+      st[4 * (256 * u + wb + lane) + ((c + (lane >> 1)) & 3)] = __builtin_bit_cast(uint4, o);
     }
   }
   __syncthreads();
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const int p = 16 * s + (lane >> 2), c = lane & 3;   // wave pixel, chunk
-    if (pix0 + wb + p < npix)
-      *reinterpret_cast<uint4*>(y + (pix0 + wb + p) * COUT + 8 * c) = st[4 * (wb + p) + ((c + (p >> 1)) & 3)];
-  }
+  for (int u = 0; u < PP; ++u)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int p = 16 * s + (lane >> 2), c = lane & 3;   // wave pixel, chunk
+      const int64_t q = pix0 + 256 * u + wb + p;
+      if (q < npix)
+        *reinterpret_cast<uint4*>(y + q * COUT + 8 * c) = st[4 * (256 * u + wb + p) + ((c + (p >> 1)) & 3)];
+    }
 }
 
 hipError_t launch_stem(DType t, const float* x, int N, int H, int W, const float* wts, int Cout,
@@ -1272,7 +1285,8 @@ hipError_t launch_stem(DType t, const float* x, int N, int H, int W, const float
   const int64_t n = (int64_t)N * H * W;
   const unsigned g = (unsigned)((n + 255) / 256);
   if (t == BF16 && Cout == 32) {
-    hipLaunchKernelGGL(stem_conv1_c32, dim3(g), dim3(256), 0, s, x, N, H, W, wts, mean, inv,
+    hipLaunchKernelGGL(stem_conv1_c32, dim3((unsigned)((n + 256 * STEM_PP - 1) / (256 * STEM_PP))),
+                       dim3(256), 0, s, x, N, H, W, wts, mean, inv,
                        (bf16_t*)y);
     return hipGetLastError();
   }
