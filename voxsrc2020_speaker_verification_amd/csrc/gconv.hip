@@ -277,16 +277,36 @@ __global__ __launch_bounds__(GC_THREADS) void gconv3x3_rows(GconvParams p) {
     for (int orow = 0; orow < RS; ++orow) {
       const int ho = hs + orow;
       if (ho >= ho1) break;   // uniform
+      auto cvt = [&](int tc) __attribute__((always_inline)) {
+        const f32x4& v = acc[orow * TPR + tc];
+        bf16x4 o;
+        o[0] = (bf16_t)v[0]; o[1] = (bf16_t)v[1];
+        o[2] = (bf16_t)v[2]; o[3] = (bf16_t)v[3];
+        return __builtin_bit_cast(uint2, o);
+      };
+      if ((p.ldy & 7) != 0) {   // (8-B aligned rows only: one 8-B store per tile)
 #pragma unroll
-      for (int tc = 0; tc < TPR; ++tc) {
-        const int oc = 16 * tc + col;
-        if (oc < Wo) {
-          const f32x4& v = acc[orow * TPR + tc];
-          bf16x4 o;
-          o[0] = (bf16_t)v[0]; o[1] = (bf16_t)v[1];
-          o[2] = (bf16_t)v[2]; o[3] = (bf16_t)v[3];
-          *reinterpret_cast<bf16x4*>(Y + ((size_t)ho * Wo + oc) * p.ldy) = o;
+        for (int tc = 0; tc < TPR; ++tc) {
+          const int oc = 16 * tc + col;
+          if (oc < Wo) *reinterpret_cast<uint2*>(Y + ((size_t)ho * Wo + oc) * p.ldy) = cvt(tc);
         }
+        continue;
+      }
+#pragma unroll
+      for (int tc = 0; tc + 1 < TPR; tc += 2) {
+        // tiles tc, tc + 1: a half-row exchange per dword gives lane (col, q)
+        // 8 contiguous channels 8 (q / 2) of tile tc + q % 2 (16-B stores)
+        const uint2 d0 = cvt(tc), d1 = cvt(tc + 1);
+        const auto s0 = __builtin_amdgcn_permlane16_swap(d0.x, d1.x, false, false);
+        const auto s1 = __builtin_amdgcn_permlane16_swap(d0.y, d1.y, false, false);
+        const int oc = 16 * (tc + (q & 1)) + col;
+        if (oc < Wo)
+          *reinterpret_cast<uint4*>(Y - 4 * q + 8 * (q >> 1) + ((size_t)ho * Wo + oc) * p.ldy) =
+              make_uint4(s0[0], s1[0], s0[1], s1[1]);
+      }
+      if constexpr (TPR % 2 == 1) {
+        const int oc = 16 * (TPR - 1) + col;
+        if (oc < Wo) *reinterpret_cast<uint2*>(Y + ((size_t)ho * Wo + oc) * p.ldy) = cvt(TPR - 1);
       }
     }
     // step j+1's rows enter the ring (staging them before the stores above,

@@ -1182,6 +1182,67 @@ __global__ __launch_bounds__(256) void stem_conv1(const float* __restrict__ x, i
   }
 }
 
+// The stem with a small even Cout (DPN68: 10): the generic kernel computed
+// 8-channel groups (16 channels for 10) and wrote each channel with its own
+// 2-byte store.  Here a thread computes its pixel's COUT channels (pairs on
+// v_pk_fma_f32, each element the fmaf chain of stem_conv1 in the same tap
+// order), packs them into COUT / 2 dwords in LDS, and the workgroup writes its
+// 256 pixels' rows (contiguous in y) as 16-B stores.  Bitwise equal to stem_conv1.
+template <int COUT>
+__global__ __launch_bounds__(256) void stem_conv1_small(const float* __restrict__ x, int N, int H,
+                                                       int W, const float* __restrict__ wts,
+                                                       const float* __restrict__ mean,
+                                                       const float* __restrict__ inv,
+                                                       bf16_t* __restrict__ y) {
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  static_assert(COUT % 2 == 0 && (256 * COUT * 2) % 16 == 0, "channel pairs, 16-B rows");
+  constexpr int DW = COUT / 2;   // dwords per pixel
+  __shared__ __attribute__((aligned(16))) float sw[9 * COUT];
+  __shared__ float sm[COUT], si[COUT];
+  __shared__ __attribute__((aligned(16))) unsigned st[256 * DW];
+  for (int i = threadIdx.x; i < 9 * COUT; i += blockDim.x) sw[i] = wts[i];
+  for (int i = threadIdx.x; i < COUT; i += blockDim.x) { sm[i] = mean[i]; si[i] = inv[i]; }
+  __syncthreads();
+  const int64_t pix0 = (int64_t)blockIdx.x * 256;
+  const int64_t npix = (int64_t)N * H * W;
+  const int64_t pix = min(pix0 + threadIdx.x, npix - 1);
+  const unsigned hw = npix < ((int64_t)1 << 32) ? (unsigned)pix % (unsigned)(H * W)
+                                                : (unsigned)(pix % ((int64_t)H * W));
+  const int hi = (int)(hw / (unsigned)W);
+  const int wi = (int)(hw - (unsigned)hi * (unsigned)W);
+  const float* xi = x + (pix - (int64_t)hw);
+  float v[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int yy = hi + t / 3 - 1, xx = wi + t % 3 - 1;
+    const bool ok = yy >= 0 && yy < H && xx >= 0 && xx < W;
+    const int yc = min(max(yy, 0), H - 1), xc = min(max(xx, 0), W - 1);
+    const float a = xi[yc * W + xc];
+    v[t] = ok ? (float)(bf16_t)a : 0.f;
+  }
+#pragma unroll
+  for (int k = 0; k < DW; ++k) {
+    f32x2 acc = {0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+      acc = __builtin_elementwise_fma(f32x2{v[t], v[t]}, *reinterpret_cast<const f32x2*>(sw + t * COUT + 2 * k), acc);
+    const f32x2 tt = (acc - f32x2{sm[2 * k], sm[2 * k + 1]}) * f32x2{si[2 * k], si[2 * k + 1]};
+    bf16x4 o = {(bf16_t)tt[0], (bf16_t)tt[1], (bf16_t)0.f, (bf16_t)0.f};
+    o = relu_bf16(o);   // == bf16(relu(x)) bit for bit (device_common.h)
+    st[threadIdx.x * DW + k] = __builtin_bit_cast(uint2, o).x;   // odd DW: conflict-free
+  }
+  __syncthreads();
+  // the block's rows are contiguous in y: 16-B pieces, a partial last block by dwords
+  const int64_t nb = min((int64_t)256, npix - pix0) * DW;   // dwords this block owns
+  unsigned* yo = reinterpret_cast<unsigned*>(y + pix0 * COUT);
+  for (int i = threadIdx.x; 4 * i < nb; i += 256) {
+    if (4 * i + 4 <= nb)
+      *reinterpret_cast<uint4*>(yo + 4 * i) = *reinterpret_cast<const uint4*>(st + 4 * i);
+    else
+      for (int e = 4 * i; e < nb; ++e) yo[e] = st[e];
+  }
+}
+
 // The stem with Cout = 32 (Res2Net): the weights as [tap][Cout] and BN in LDS
 // are read 4 channels per 16-B broadcast (ds_read_b128) instead of one float per
 // FMA -- the per-FMA LDS reads bounded the generic kernel (122 us at 256 x 200 x
@@ -1287,6 +1348,11 @@ hipError_t launch_stem(DType t, const float* x, int N, int H, int W, const float
   if (t == BF16 && Cout == 32) {
     hipLaunchKernelGGL(stem_conv1_c32, dim3((unsigned)((n + 256 * STEM_PP - 1) / (256 * STEM_PP))),
                        dim3(256), 0, s, x, N, H, W, wts, mean, inv,
+                       (bf16_t*)y);
+    return hipGetLastError();
+  }
+  if (t == BF16 && Cout == 10) {
+    hipLaunchKernelGGL(stem_conv1_small<10>, dim3(g), dim3(256), 0, s, x, N, H, W, wts, mean, inv,
                        (bf16_t*)y);
     return hipGetLastError();
   }
