@@ -754,6 +754,7 @@ __global__ __launch_bounds__(DB_THREADS) void dpn_down_rows(DpnDownParams p) {
     lofs[m] = ((chunk >> 1) * SPW + 2 * slot_of(S * col + kx + (S == 2 ? 1 : 0)) + (chunk & 1)) * 16;
   }
   bf16_t* __restrict__ Y = reinterpret_cast<bf16_t*>(p.y) + (size_t)n * Ho * Wo * p.ldy + c0 + 16 * wave + 4 * g;
+  const bool wide = (p.ldy & 7) == 0;   // 16-B aligned rows
   auto gconv_row = [&](int o) __attribute__((always_inline)) {
     const int wr = S == 2 ? 2 * o : o - 1;   // window row 0
     const int r0 = __builtin_amdgcn_readfirstlane(ring_off(wr));
@@ -776,14 +777,37 @@ __global__ __launch_bounds__(DB_THREADS) void dpn_down_rows(DpnDownParams p) {
         acc[t] = mfma_step(ag[m], bv, acc[t]);
       }
     }
-#pragma unroll
-    for (int t = 0; t < DD_TPO; ++t) {
-      const int oc = 16 * t + col;
+    auto cvt = [&](int t) __attribute__((always_inline)) {
       bf16x4 o4;
 #pragma unroll
       for (int e = 0; e < 4; ++e) o4[e] = (bf16_t)acc[t][e];
-      void* d = oc < Wo ? (void*)(Y + ((size_t)o * Wo + oc) * p.ldy) : (void*)&g_db_sink[lane];
-      *reinterpret_cast<bf16x4*>(d) = o4;
+      return __builtin_bit_cast(uint2, o4);
+    };
+    if (wide) {
+      // tiles t, t + 1: a half-row exchange per dword gives lane (col, g) 8
+      // contiguous channels 8 (g / 2) of tile t + g % 2, one 16-B store
+      // (8-B stores were 16 pixels x 32 B per instruction)
+#pragma unroll
+      for (int t = 0; t + 1 < DD_TPO; t += 2) {
+        const uint2 d0 = cvt(t), d1 = cvt(t + 1);
+        const auto s0 = __builtin_amdgcn_permlane16_swap(d0.x, d1.x, false, false);
+        const auto s1 = __builtin_amdgcn_permlane16_swap(d0.y, d1.y, false, false);
+        const int oc = 16 * (t + (g & 1)) + col;
+        if (oc < Wo)
+          *reinterpret_cast<uint4*>(Y - 4 * g + 8 * (g >> 1) + ((size_t)o * Wo + oc) * p.ldy) =
+              make_uint4(s0[0], s1[0], s0[1], s1[1]);
+      }
+      if constexpr (DD_TPO % 2 == 1) {
+        const int oc = 16 * (DD_TPO - 1) + col;
+        if (oc < Wo) *reinterpret_cast<uint2*>(Y + ((size_t)o * Wo + oc) * p.ldy) = cvt(DD_TPO - 1);
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < DD_TPO; ++t) {
+        const int oc = 16 * t + col;
+        void* d = oc < Wo ? (void*)(Y + ((size_t)o * Wo + oc) * p.ldy) : (void*)&g_db_sink[lane];
+        *reinterpret_cast<uint2*>(d) = cvt(t);
+      }
     }
   };
 
