@@ -1648,18 +1648,37 @@ __global__ __launch_bounds__((S2FusedCfg<CI, WID, S, WIN>::NT)) void s2_fused(Ch
           for (int j = 0; j < PT; ++j) bc[j] = bn[j];
           __builtin_amdgcn_sched_barrier(0);   // reads stay one k-step ahead
         }
+        auto ycv = [&](int j) __attribute__((always_inline)) {
+          bf16x4 y;
+          {
+            const f32x4 t = (acc[j] + m) * sc;
 #pragma unroll
-        for (int j = 0; j < PT; ++j) {
-          const int wo = 16 * j + col;
-          if (co < WID && wo < Wo) {
-            bf16x4 y;
-            {
-              const f32x4 t = (acc[j] + m) * sc;
+            for (int e = 0; e < 4; ++e) y[e] = (bf16_t)t[e];
+          }
+          return __builtin_bit_cast(uint2, relu_bf16(y));
+        };
+        bf16_t* const brow = Bo + (imgo + (size_t)ho * Wo) * q.ldb + ck * WID;
+        if ((q.ldb & 7) == 0) {
+          // tiles j, j + 1: a half-row exchange per dword gives lane (col, g) 8
+          // contiguous channels 16 ci + 8 (g / 2) of tile j + g % 2 (16-B stores)
 #pragma unroll
-              for (int e = 0; e < 4; ++e) y[e] = (bf16_t)t[e];
-            }
-            y = relu_bf16(y);
-            *reinterpret_cast<bf16x4*>(Bo + (imgo + (size_t)ho * Wo + wo) * q.ldb + ck * WID + co) = y;
+          for (int j = 0; j + 1 < PT; j += 2) {
+            const uint2 d0 = ycv(j), d1 = ycv(j + 1);
+            const auto s0 = __builtin_amdgcn_permlane16_swap(d0.x, d1.x, false, false);
+            const auto s1 = __builtin_amdgcn_permlane16_swap(d0.y, d1.y, false, false);
+            const int wo = 16 * (j + (g & 1)) + col, cq = 16 * ci + 8 * (g >> 1);
+            if (cq < WID && wo < Wo)
+              *reinterpret_cast<uint4*>(brow + (size_t)wo * q.ldb + cq) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+          }
+          if constexpr (PT % 2 == 1) {
+            const int wo = 16 * (PT - 1) + col;
+            if (co < WID && wo < Wo) *reinterpret_cast<uint2*>(brow + (size_t)wo * q.ldb + co) = ycv(PT - 1);
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < PT; ++j) {
+            const int wo = 16 * j + col;
+            if (co < WID && wo < Wo) *reinterpret_cast<uint2*>(brow + (size_t)wo * q.ldb + co) = ycv(j);
           }
         }
       } else if (!(VOX_DBG(q) & 4)) {
