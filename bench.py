@@ -258,9 +258,70 @@ def cpu_baseline(model, feat_dim, T, blob, budget_s=15.0):
                       f"oracle/cpu/voxcpu.cpp fp32 C++/OpenMP, {threads} threads: {why})"}
 
 
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` started without a launcher: start N rank processes
+    of this same script (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, one per
+    GPU, as torchrun would and as eval_inference_model.sh:29-36 starts
+    `num_gpus` tf_extract.py processes) and return the worst exit code.  Runs
+    in the parent before anything touches the GPU; the parent never execs."""
+    import subprocess
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    codes = []
+    try:
+        for p in procs:
+            codes.append(p.wait())
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    bad = [c for c in codes if c != 0]
+    return bad[0] if bad else 0
+
+
+def stub_rank(args, world, rank):
+    """--stub-extractor: the rank/launch logic of main() on the CPU (gloo, a
+    numpy stand-in for the forward) so the CPU tests can check that `--gpus N`
+    runs N ranks and that the line's n_gpus is the ranks that ran."""
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    x = bench_features(2, args.frames, args.feat_dim, rank)
+    out = torch.from_numpy(np.concatenate([x.mean(1), x.std(1)], 1).astype(np.float32))
+    gathered = [torch.empty_like(out) for _ in range(world)]
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        dist.all_gather(gathered, out)
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    pid = torch.tensor([os.getpid()], dtype=torch.int64)
+    pids = [torch.zeros_like(pid) for _ in range(world)]
+    dist.all_gather(pids, pid)
+    if rank == 0:
+        print(json.dumps({"metric": "stub", "n_gpus": world,
+                          "ranks_ran": len({int(p.item()) for p in pids}), "steps": args.steps,
+                          "value": 2 * world * args.steps / max(float(el.item()), 1e-9)}))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU): without a launcher, N > 1 starts N rank "
+                         "processes; under torchrun it must equal WORLD_SIZE")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--model", default="res2net50_w24_s4_c32")
@@ -271,14 +332,32 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dump-ops", action="store_true", help="print per-op timing to stderr")
     ap.add_argument("--cache-dir", default=os.environ.get("VOXEMB_CACHE", "/tmp/voxemb_cache"))
+    ap.add_argument("--stub-extractor", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
 
-    import torch
-    import torch.distributed as dist
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:
+            # no launcher: become the launcher (before any GPU call in this process)
+            sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    elif int(os.environ["WORLD_SIZE"]) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE="
+              f"{os.environ['WORLD_SIZE']} ranks; refusing to report a line whose n_gpus "
+              f"would not be the ranks that ran", file=sys.stderr)
+        sys.exit(2)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.stub_extractor:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+        return stub_rank(args, world, rank)
+
+    import torch
+    import torch.distributed as dist
+
     # under torchrun (WORLD_SIZE set) the RCCL path runs even at one rank: the
     # per-step all-gather of the embeddings (cohort assembly) is in the timed region
     dist_on = world > 1 or "WORLD_SIZE" in os.environ

@@ -34,7 +34,7 @@ def _items(n_utts):
     return feats, items
 
 
-def _worker(rank, world, port, outdir, n_utts, streamed=False):
+def _worker(rank, world, port, outdir, n_utts, streamed=False, all_gather=False):
     import torch.distributed as dist
     from voxsrc2020_speaker_verification_amd import dp_extract
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
@@ -50,14 +50,21 @@ def _worker(rank, world, port, outdir, n_utts, streamed=False):
             table = stream.ChunkTable(shard(kaldi.read_scp(os.path.join(outdir, "feats.scp")), r, w), 2)
             return stream.extract_stream(
                 table, lambda b: stream.SyncRunner(table, _fake_embed, cmn=False), 3)
-    dp_extract.run(rank, world, items, _fake_embed, 8, os.path.join(outdir, "xvector"),
-                   batch=3, cohort_spk2utt=spk2utt, extract_shard=shard_fn)
+    keys, emb = dp_extract.run(rank, world, items, _fake_embed, 8, os.path.join(outdir, "xvector"),
+                               batch=3, cohort_spk2utt=spk2utt, extract_shard=shard_fn,
+                               all_gather=all_gather)
+    # rank 0 receives everything; the others only with all_gather
+    got = len(keys) if emb is None else emb.shape[0]
+    with open(os.path.join(outdir, f"recv{rank}"), "w") as f:
+        f.write(f"{len(keys)} {got}")
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n_utts,streamed", [(2, 11, False), (3, 7, False), (2, 11, True)])
-def test_dp_extract_gloo(tmp_path, world, n_utts, streamed):
+@pytest.mark.parametrize("world,n_utts,streamed,all_gather",
+                         [(2, 11, False, False), (3, 7, False, True), (3, 7, False, False),
+                          (2, 11, True, False)])
+def test_dp_extract_gloo(tmp_path, world, n_utts, streamed, all_gather):
     import torch.multiprocessing as mp
     from voxsrc2020_speaker_verification_amd import kaldi
     from voxsrc2020_speaker_verification_amd.extract import embed_utterances
@@ -71,8 +78,11 @@ def test_dp_extract_gloo(tmp_path, world, n_utts, streamed):
                 rec, off = kaldi.format_mat_flt(k, m)
                 fs.write(f"{k} {tmp_path / 'feats.ark'}:{fa.tell() + off}\n")
                 fa.write(rec)
-    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), n_utts, streamed), nprocs=world,
-             join=True)
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), n_utts, streamed, all_gather),
+             nprocs=world, join=True)
+    recv = [open(tmp_path / f"recv{r}").read() for r in range(world)]
+    full = f"{n_utts} {n_utts}"
+    assert recv == [full] * world if all_gather else recv == [full] + ["0 0"] * (world - 1)
     # merged ark is byte-identical to the concatenation of the per-rank arks
     cat = b"".join(open(tmp_path / f"xvector.{r + 1}.ark", "rb").read() for r in range(world))
     assert open(tmp_path / "xvector.ark", "rb").read() == cat
@@ -83,6 +93,12 @@ def test_dp_extract_gloo(tmp_path, world, n_utts, streamed):
         np.testing.assert_array_equal(got[k], e)
     coh = np.load(tmp_path / "xvector.cohort.npy")
     assert coh.shape == (3, 8)
+    # the vectorised cohort == snorm.py's per-utterance dict path, bit for bit
+    from voxsrc2020_speaker_verification_amd import scoring
+    spk = scoring.speaker_xvectors({k: scoring.l2norm(v, axis=0) for k, v in got.items()},
+                                   scoring.read_spk2utt(str(tmp_path / "spk2utt")))
+    assert np.array_equal(coh, np.array(list(spk.values()), np.float32))
+    assert open(tmp_path / "xvector.cohort.keys").read().split() == list(spk)
 
 
 def _failing_worker(rank, world, port, outdir):

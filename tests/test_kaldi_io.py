@@ -121,3 +121,32 @@ def test_sliding_cmn_non_centered():
     from voxsrc2020_speaker_verification_amd.kaldi import sliding_cmn
     x = np.random.default_rng(3).standard_normal((400, 5)).astype(np.float32)
     assert np.array_equal(sliding_cmn(x, 300, center=False), ref(x, 300, center=False))
+
+
+def test_write_many_bytes_equal_per_record_writer(tmp_path):
+    """VectorWriter.write_many (the merged-ark writer of dp_extract) writes the
+    same ark and scp bytes as one write() per vector (vox_format_vec_flt, whose
+    records equal kaldi_io.write_vec_flt's, golden above)."""
+    from voxsrc2020_speaker_verification_amd.kaldi import VectorWriter
+    rng = np.random.default_rng(3)
+    keys = [f"id{i:05d}-utt_{i * 7}" for i in range(37)] + ["x"]
+    emb = rng.standard_normal((len(keys), 256)).astype(np.float32)
+    with VectorWriter(str(tmp_path / "a")) as w:
+        for k, v in zip(keys, emb):
+            w.write(k, v)
+    with VectorWriter(str(tmp_path / "b")) as w:
+        w.write("first", emb[0])               # offsets continue after earlier records
+        w.write_many(keys, emb)
+    with VectorWriter(str(tmp_path / "c")) as w:
+        w.write("first", emb[0])
+        for k, v in zip(keys, emb):
+            w.write(k, v)
+    assert (tmp_path / "b.ark").read_bytes() == (tmp_path / "c.ark").read_bytes()
+    assert ((tmp_path / "b.scp").read_text().replace("/b.ark", "/c.ark")
+            == (tmp_path / "c.scp").read_text())
+    with VectorWriter(str(tmp_path / "d")) as w:
+        w.write_many(keys, emb)
+    assert (tmp_path / "d.ark").read_bytes() == (tmp_path / "a.ark").read_bytes()
+    with pytest.raises(ValueError):
+        with VectorWriter(str(tmp_path / "e")) as w:
+            w.write_many(["bad key"], emb[:1])

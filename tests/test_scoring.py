@@ -115,3 +115,28 @@ def test_projection_weight_cohort_matches_reference(tmp_path):
     got = [l.split()[2] for l in open(asn_f)]
     # the reference prints numpy float32 scalars: the same text
     assert got == [str(np.float32(v)) for v in exp["asnorm"]]
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_speaker_means_bit_exact_vs_dict_path(seed):
+    """scoring.speaker_means (dp_extract's cohort assembly, no per-utterance
+    Python step) == snorm.py's path speaker_xvectors({k: l2norm(v)}) bit for
+    bit, incl. repeated keys, utterances under two speakers, utterances of no
+    speaker and spk2utt entries never extracted."""
+    from voxsrc2020_speaker_verification_amd import scoring as S
+    rng = np.random.default_rng(seed)
+    n = int(rng.integers(1, 300))
+    D = int(rng.choice([1, 8, 33, 256]))
+    keys = [f"u{int(rng.integers(0, 2 * n))}" for _ in range(n)]
+    emb = (rng.standard_normal((n, D)) * rng.uniform(0.1, 50)).astype(np.float32)
+    spk2utt = {}
+    for k in sorted(set(keys)) + ["never1", "never2"]:
+        if rng.random() < 0.1:
+            continue
+        for s in rng.choice(int(rng.integers(1, 20)), size=int(rng.integers(1, 3))):
+            spk2utt.setdefault(f"s{s}", []).append(k)
+    ref = S.speaker_xvectors({k: S.l2norm(v, axis=0) for k, v in zip(keys, emb)}, spk2utt)
+    ks, m = S.speaker_means(keys, emb, spk2utt)
+    assert ks == list(ref)
+    r = np.array(list(ref.values()), np.float32).reshape(len(ref), D)
+    assert m.dtype == np.float32 and np.array_equal(r.view(np.uint32), m.view(np.uint32))

@@ -1,14 +1,16 @@
-"""Data-parallel extraction: one process per GPU + one RCCL all-gather.
+"""Data-parallel extraction: one process per GPU + one RCCL gather to rank 0.
 
 Reference: tensorflow/eval_inference_model.sh:27-40 starts `num_gpus`
 independent tf_extract.py processes (CUDA_VISIBLE_DEVICES=i-1) on the
 contiguous shards data/<set>/<N>-split/feats.<i>.scp and then "gathers" with
 `cat xvector.{1..N}.ark > xvector.ark`.  Here each rank extracts the
 split_scp.pl shard of the scp (or reads the reference's pre-split shard
-file), then the per-rank embedding matrices are assembled on every rank with
-one all-gather over RCCL/xGMI (backend "nccl"; "gloo" for CPU tests).  Rank 0
-writes the merged ark/scp in shard order, i.e. byte-identical to the `cat`,
-plus (optionally) the cohort speaker-mean matrix for AS-norm (snorm.py:45-67).
+file), then the per-rank embedding matrices are assembled on rank 0 with one
+gather over RCCL/xGMI (backend "nccl"; "gloo" for CPU tests; `--all-gather`
+delivers them to every rank instead).  Rank 0 writes the merged ark/scp in
+shard order, i.e. byte-identical to the `cat`, plus (optionally) the cohort
+speaker-mean matrix for AS-norm (snorm.py:45-67), formed without a
+per-utterance Python step (scoring.speaker_means; tools/bench_cohort.py).
 
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 -m \\
         voxsrc2020_speaker_verification_amd.dp_extract --pb-file m.blob \\
@@ -25,12 +27,18 @@ import sys
 import numpy as np
 
 
-def gather_embeddings(keys, emb, group=None, device=None):
-    """All-gather variable-sized [n_r, D] float32 matrices (+ their keys) from
-    every rank; returns (all_keys, [sum n_r, D]) in rank order."""
+def gather_embeddings(keys, emb, group=None, device=None, dst=None):
+    """Gather variable-sized [n_r, D] float32 matrices (+ their keys) from every
+    rank, in rank order.  dst=None: all-gather, every rank returns (all_keys,
+    [sum n_r, D]); dst=r: only rank r receives them (one RCCL gather of the
+    matrices, the keys pickled to r alone) and the other ranks return
+    ([], None) -- the merged ark and the cohort are rank 0's alone, so at
+    VoxCeleb2-dev scale (1.09 M x 256 = 1.1 GB) nothing is copied to ranks
+    that would drop it."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
     dim = emb.shape[1]
     dev = device if device is not None else torch.device("cpu")
     n = torch.tensor([emb.shape[0]], dtype=torch.int64, device=dev)
@@ -41,13 +49,26 @@ def gather_embeddings(keys, emb, group=None, device=None):
     buf = torch.zeros((mx, dim), dtype=torch.float32, device=dev)
     if emb.shape[0]:
         buf[:emb.shape[0]] = torch.from_numpy(np.ascontiguousarray(emb)).to(dev)
-    parts = [torch.empty_like(buf) for _ in range(world)]
-    dist.all_gather(parts, buf, group=group)
-    key_lists = [None] * world
-    dist.all_gather_object(key_lists, list(keys), group=group)
-    mats = [p[:c].cpu().numpy() for p, c in zip(parts, counts)]
+    recv = dst is None or rank == dst
+    if recv:
+        # one receive slab, filled in rank order: no per-part host copies
+        slab = torch.empty((world, mx, dim), dtype=torch.float32, device=dev)
+        parts = list(slab.unbind(0))
+    if dst is None:
+        dist.all_gather(parts, buf, group=group)
+        key_lists = [None] * world
+        dist.all_gather_object(key_lists, list(keys), group=group)
+    else:
+        dist.gather(buf, parts if recv else None, dst=dst, group=group)
+        key_lists = [None] * world if recv else None
+        dist.gather_object(list(keys), key_lists, dst=dst, group=group)
+    if not recv:
+        return [], None
+    host = slab.cpu().numpy()
     all_keys = [k for kl in key_lists for k in kl]
-    return all_keys, (np.concatenate(mats, 0) if mats else np.zeros((0, dim), np.float32))
+    if all(c == mx for c in counts):
+        return all_keys, host.reshape(world * mx, dim)
+    return all_keys, np.concatenate([host[r, :c] for r, c in enumerate(counts)], 0)
 
 
 def rank_failures(failed, device=None, group=None):
@@ -112,7 +133,7 @@ def completed_shard(wspec, rank, keys, dim, tag=None):
 
 def run(rank, world, scp_items, embed_fn, dim, wspec, shard_file=None, batch=64,
         device=None, write_per_rank=True, cohort_spk2utt=None, resume=False, shard_keys=None,
-        tag=None, extract_shard=None):
+        tag=None, extract_shard=None, all_gather=False):
     """The per-rank body (also used by the gloo tests with a fake embedder).
     scp_items: full list of (key, feat) is NOT required -- each rank only
     decodes its own shard: `scp_items` is a callable(rank, world) -> list of
@@ -123,7 +144,10 @@ def run(rank, world, scp_items, embed_fn, dim, wspec, shard_file=None, batch=64,
     (run_tag) written beside each per-rank pair and required to match on
     resume.  extract_shard: callable(rank, world) -> (keys, [n, dim]
     embeddings) that replaces scp_items + embed_fn (the CLI's streaming GPU
-    pipeline, stream.extract_entries: the shard is never decoded whole)."""
+    pipeline, stream.extract_entries: the shard is never decoded whole).
+    all_gather: every rank receives every embedding (returned everywhere);
+    default False gathers to rank 0 only, the one rank that writes the merged
+    ark and the cohort; the other ranks return ([], None)."""
     from .extract import embed_utterances, write_vectors
     err = None
     try:
@@ -157,14 +181,14 @@ def run(rank, world, scp_items, embed_fn, dim, wspec, shard_file=None, batch=64,
         if err is not None:
             raise err
         raise RuntimeError(f"extraction failed on rank(s) {failed}; rank {rank} aborts too")
-    all_keys, all_emb = gather_embeddings(keys, emb, device=device)
+    all_keys, all_emb = gather_embeddings(keys, emb, device=device,
+                                          dst=None if all_gather else 0)
     if rank == 0 and wspec:
         write_vectors(wspec, all_keys, all_emb)           # == cat xvector.{1..N}.ark
         if cohort_spk2utt:
-            from .scoring import l2norm, read_spk2utt, speaker_xvectors
-            xv = {k: l2norm(v, axis=0) for k, v in zip(all_keys, all_emb)}
-            spk = speaker_xvectors(xv, read_spk2utt(cohort_spk2utt))
-            np.save(wspec + ".cohort.npy", np.array(list(spk.values()), np.float32))
+            from .scoring import read_spk2utt, speaker_means
+            spk, cohort = speaker_means(all_keys, all_emb, read_spk2utt(cohort_spk2utt))
+            np.save(wspec + ".cohort.npy", cohort.astype(np.float32, copy=False))
             with open(wspec + ".cohort.keys", "w") as f:
                 f.write("\n".join(spk) + "\n")
     return all_keys, all_emb
@@ -185,6 +209,8 @@ def main(argv=None):
     ap.add_argument("--reader-threads", type=int, default=None)
     ap.add_argument("--resume", action="store_true",
                     help="reuse per-rank xvector.<i>.ark/.scp that already hold the rank's shard")
+    ap.add_argument("--all-gather", action="store_true",
+                    help="deliver every embedding to every rank (default: rank 0 only)")
     a = ap.parse_args(argv)
 
     import torch
@@ -218,7 +244,8 @@ def main(argv=None):
             device=torch.device("cuda", local), cohort_spk2utt=a.cohort_spk2utt,
             resume=a.resume, shard_keys=keys, tag=run_tag(a.pb_file, a.precision),
             extract_shard=lambda r, w: extract_entries(entries(r, w), lanes, a.batch,
-                                                       threads=a.reader_threads))
+                                                       threads=a.reader_threads),
+            all_gather=a.all_gather)
     finally:
         for ex in lanes:
             ex.close()

@@ -81,8 +81,8 @@ def open_lanes(pb_file, device, precision, lanes):
 def write_vectors(base, keys, emb, atomic=False):
     from .kaldi import VectorWriter
     with VectorWriter(base, atomic=atomic) as w:
-        for k, v in zip(keys, emb):
-            w.write(k, v)
+        if len(keys):
+            w.write_many(keys, np.asarray(emb, np.float32).reshape(len(keys), -1))
 
 
 def main(argv=None):

@@ -177,6 +177,36 @@ class VectorWriter:
         self._ark.write(rec)
         self._scp.write(f"{key} {self.ark_path}:{pos + off}\n")
 
+    def write_many(self, keys, emb):
+        """write() for every (key, row) of a [n, dim] matrix: the same bytes as
+        vox_format_vec_flt per record, assembled here in one pass (a 1.09 M
+        utterance merged ark is ~1 s instead of one native call per vector)."""
+        emb = np.ascontiguousarray(emb, dtype=np.float32)
+        if emb.ndim != 2 or len(keys) != emb.shape[0]:
+            raise ValueError("expected one key per row of a 2-D matrix")
+        mid = np.frombuffer(b" \0BFV \4" + np.uint32(emb.shape[1]).tobytes(), np.uint8)
+        rb = emb.shape[1] * 4
+        kbs = [k.encode("utf-8") for k in keys]
+        for kb in kbs:
+            if not kb or b" " in kb or b"\0" in kb:
+                raise ValueError(f"key must be non-empty without spaces: {kb!r}")
+        klen = np.fromiter(map(len, kbs), dtype=np.int64, count=len(kbs))
+        rec = klen + len(mid) + rb
+        start = self._ark.tell() + np.concatenate([[0], np.cumsum(rec)[:-1]])
+        # runs of equal-length keys (all of VoxCeleb's) are records of one size:
+        # each run is laid out as one [run, record] byte matrix
+        cut = np.flatnonzero(np.diff(klen)) + 1
+        data = emb.view(np.uint8).reshape(len(kbs), rb)
+        for a, b in zip(np.r_[0, cut], np.r_[cut, len(kbs)]):
+            L = int(klen[a])
+            m = np.empty((b - a, L + len(mid) + rb), np.uint8)
+            m[:, :L] = np.frombuffer(b"".join(kbs[a:b]), np.uint8).reshape(b - a, L)
+            m[:, L:L + len(mid)] = mid
+            m[:, L + len(mid):] = data[a:b]
+            self._ark.write(m.data)
+        self._scp.write("".join(f"{k} {self.ark_path}:{o}\n"
+                                for k, o in zip(keys, (start + klen + 1).tolist())))
+
     def close(self):
         if self._ark:
             self._ark.close()
