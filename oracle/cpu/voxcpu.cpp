@@ -18,8 +18,10 @@
 // block) as [K][16]; register tiles of 12 pixels x 32 couts (AVX-512, picked
 // at run time when the host has it) or 6 x 16 (AVX2 + FMA, the -march=x86-64-v3
 // baseline); OpenMP over (pixel block, cout block); BN / ReLU / residual /
-// the next split's addend fused into the conv epilogue.  BN is applied as
-// (x - mean) * (1 / sqrt(var + eps)), TF's formula, everything in float32.
+// the next split's addend fused into the conv epilogue.  The 4-D BNs are
+// applied as (x - mean) * (1 / sqrt(var + eps)) (TF's fused kernel), the 2-D
+// head BNs as x * inv + (-mean * inv) (tf.nn.batch_normalization, bn2d);
+// everything in float32.
 // Measured in this build container (8 Sapphire Rapids cores): res2net50 80x200
 // 15.7 utt/s = 350 GFLOP/s (AVX-512), 9.3 utt/s (AVX2); the numpy oracle ~6.6.
 #include <immintrin.h>
@@ -84,7 +86,17 @@ struct Conv {
 
 struct BN {
   std::vector<float> mean, inv;
+  std::vector<float> nmi;  // -mean * inv: the 2-D head's non-fused form (bn2d)
 };
+
+// tf.nn.batch_normalization, what TF1 runs for the 2-D head BNs
+// (tf.compat.v1.layers fuses 4-D inputs only): x * inv + (-mean * inv), a Mul
+// and an Add, two roundings -- the volatile keeps gcc from contracting them
+// to an FMA under -march=x86-64-v3
+static inline float bn2d(float x, float inv, float nmi) {
+  volatile float t = x * inv;
+  return t + nmi;
+}
 
 Conv make_conv(const Tensor& t, int groups) {
   Conv c;
@@ -455,6 +467,10 @@ int load_weights(voxcpu_model* m, const std::vector<Tensor>& ts) {
   if (!h1m || !h1v || !dk || !h2m || !h2v) return fail("blob exhausted (head)");
   m->hb1 = make_bn(*h1m, *h1v, m->eps2);
   m->hb2 = make_bn(*h2m, *h2v, m->eps2);
+  for (BN* b : {&m->hb1, &m->hb2}) {
+    b->nmi.resize(b->mean.size());
+    for (size_t i = 0; i < b->mean.size(); ++i) b->nmi[i] = -b->mean[i] * b->inv[i];
+  }
   m->dense = dk->data;
   m->pooled = dk->shape[0];
   m->out_dim = dk->shape[1];
@@ -533,14 +549,14 @@ void head(const voxcpu_model* m, const float* pooled, int n, float* out) {
 #pragma omp parallel for schedule(static)
   for (int i = 0; i < n; ++i) {
     std::vector<float> z(D);
-    for (int d = 0; d < D; ++d) z[d] = (pooled[(size_t)i * D + d] - m->hb1.mean[d]) * m->hb1.inv[d];
+    for (int d = 0; d < D; ++d) z[d] = bn2d(pooled[(size_t)i * D + d], m->hb1.inv[d], m->hb1.nmi[d]);
     std::vector<float> acc(O, 0.f);
     for (int d = 0; d < D; ++d) {
       const float a = z[d];
       const float* wr = m->dense.data() + (size_t)d * O;
       for (int o = 0; o < O; ++o) acc[o] += a * wr[o];
     }
-    for (int o = 0; o < O; ++o) out[(size_t)i * O + o] = (acc[o] - m->hb2.mean[o]) * m->hb2.inv[o];
+    for (int o = 0; o < O; ++o) out[(size_t)i * O + o] = bn2d(acc[o], m->hb2.inv[o], m->hb2.nmi[o]);
   }
 }
 

@@ -154,6 +154,19 @@ def batch_norm(x, mean, var, eps=None):
     return ((x - mean.astype(np.float32)) * inv).astype(np.float32)
 
 
+def batch_norm_2d(x, mean, var, eps):
+    """The 2-D head BNs: tf.compat.v1.layers.batch_normalization picks the fused
+    kernel only for 4-D inputs, so on the [N, D] head TF1 runs
+    tf.nn.batch_normalization, x * inv + (-mean * inv) with inv = rsqrt(var +
+    eps) (offset and scale None: center=False, scale=False), as a Mul and an
+    Add -- two float32 roundings.  inv here is the correctly rounded 1/sqrt;
+    TF's Eigen rsqrt (EIGEN_FAST_MATH) may differ in the last bit (TF absent:
+    unpinned)."""
+    inv = (np.float32(1.0) / np.sqrt(var.astype(np.float32) + np.float32(eps))).astype(np.float32)
+    nmi = (-mean.astype(np.float32) * inv).astype(np.float32)
+    return ((x.astype(np.float32) * inv).astype(np.float32) + nmi).astype(np.float32)
+
+
 def relu(x):
     return np.maximum(x, np.float32(0))
 
@@ -206,9 +219,9 @@ def head(x, t, names):
     """BN(2-D) -> dense (no bias) -> BN(2-D) -> 'outputs'
     (res2net_model.py:239-242, tdnn_model.py:148-153, dpn_model.py:163-167)."""
     bn1, dense, bn2 = names
-    x = batch_norm(x, t[bn1 + "/moving_mean"], t[bn1 + "/moving_variance"], BN_EPS_2D)
+    x = batch_norm_2d(x, t[bn1 + "/moving_mean"], t[bn1 + "/moving_variance"], BN_EPS_2D)
     x = (x @ t[dense]).astype(np.float32)
-    return batch_norm(x, t[bn2 + "/moving_mean"], t[bn2 + "/moving_variance"], BN_EPS_2D)
+    return batch_norm_2d(x, t[bn2 + "/moving_mean"], t[bn2 + "/moving_variance"], BN_EPS_2D)
 
 
 # ----------------------------------------------------------------- backbones
@@ -244,9 +257,9 @@ def _head_layer(p):
     assert p.done()
 
     def f(x):
-        x = batch_norm(x, m1, v1, BN_EPS_2D)
+        x = batch_norm_2d(x, m1, v1, BN_EPS_2D)
         x = _mm(x, dense)
-        return batch_norm(x, m2, v2, BN_EPS_2D)
+        return batch_norm_2d(x, m2, v2, BN_EPS_2D)
     return f
 
 

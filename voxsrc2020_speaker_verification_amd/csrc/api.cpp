@@ -532,6 +532,21 @@ static int make_bn(const HostTensor& bm, const HostTensor& bv, float eps, BNW& o
   return VOX_OK;
 }
 
+// tf.nn.batch_normalization (the non-fused inference BN TF1 uses for a 2-D
+// input, models.py:62-67 via tf.compat.v1.layers): y = x * inv + (-mean * inv).
+// Overwrites a BN's mean table with -mean * inv, inv computed exactly as in
+// make_bn / make_conv
+static int bn_nonfused_offsets(const HostTensor& bm, const HostTensor& bv, float eps, DevBuf& dst) {
+  const int C = (int)bm.data.size();
+  std::vector<float> nmi(C);
+  for (int c = 0; c < C; ++c) {
+    const float inv = 1.0f / std::sqrt(bv.data[c] + eps);
+    nmi[c] = -bm.data[c] * inv;
+  }
+  HIPCHK(hipMemcpy(dst.p, nmi.data(), C * 4, hipMemcpyHostToDevice));
+  return VOX_OK;
+}
+
 struct Cursor {
   const std::vector<HostTensor>& ts;
   size_t i = 0;
@@ -652,6 +667,10 @@ static int load_weights(vox_model* m, const std::vector<HostTensor>& ts) {
   HostTensor dk4 = *dk;  // [D, out] -> HWIO [1,1,D,out]
   dk4.shape = {1, 1, dk->shape[0], dk->shape[1]};
   if ((rc = make_conv(m, dk4, 1, h2m, h2v, m->eps2, F32, m->head))) return rc;
+  // both head BNs are 2-D, so TF1 runs them non-fused: their mean tables hold
+  // -mean * inv for the kernels' bn2d (EPI_BN2D)
+  if ((rc = bn_nonfused_offsets(*h1m, *h1v, m->eps2, *m->head_bn1.mean))) return rc;
+  if ((rc = bn_nonfused_offsets(*h2m, *h2v, m->eps2, *m->head.mean))) return rc;
   m->pooled = dk->shape[0];
   m->out_dim = dk->shape[1];
   if (cur.i != ts.size()) return fail(VOX_EIO, "blob has trailing tensors");
@@ -993,7 +1012,7 @@ static void emit_head(Builder& B, const float* pooled, int n, float* out) {
   r.kind = OP_HEAD;
   r.type = 1;
   r.part = part; r.S = S; r.M = n; r.coutp = hw.coutp; r.cout = hw.cout;
-  r.flags = EPI_AFFINE;
+  r.flags = EPI_BN2D;
   r.mean = (const float*)hw.mean->p; r.inv = (const float*)hw.inv->p;
   r.out = out; r.ldo = hw.cout;
   r.bytes = 4.0 * ((double)S * n * hw.cout + (double)n * hw.cout);

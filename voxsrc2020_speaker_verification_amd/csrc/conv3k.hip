@@ -139,6 +139,10 @@ struct KsCfg {
   static constexpr int XPC = XZB / 1024;
   static constexpr int LDS = 2 * WBUF + KS_XCH + XZB + 2 * KS_C * 4;
   static_assert(XZB % 1024 == 0, "x pieces");
+  // the next tile's window is issued at the first pass's k16-steps s % 6 == 3
+  // (fill() in the kernel): one piece per wave at each, so every piece must
+  // have a slot there or nwin no longer matches what was issued
+  static_assert(WPC <= KS_NW * ((KS_SH - 4) / 6 + 1), "window fill schedule too short");
   static_assert(LDS <= 163840, "LDS");
 };
 

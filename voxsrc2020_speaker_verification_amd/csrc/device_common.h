@@ -9,6 +9,14 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// TF1 nn.batch_normalization at inference (the 2-D head BNs, non-fused):
+// x * inv + (-mean * inv) as two roundings -- its Mul and Add graph ops --
+// never contracted to an FMA; nmi = -mean * inv is precomputed at load
+__device__ __forceinline__ float bn2d(float x, float inv, float nmi) {
+#pragma clang fp contract(off)
+  return x * inv + nmi;
+}
+
 __device__ __forceinline__ bf16x8 ld16(const bf16_t* p) {
   uint4 u = *reinterpret_cast<const uint4*>(p);
   return __builtin_bit_cast(bf16x8, u);

@@ -348,17 +348,41 @@ struct FirstError {
   }
 };
 
+// body(i) for i < n on up to `threads` workers (the caller is one of them).
+// Nothing escapes to the extern "C" callers: an exception in a body (e.g.
+// std::bad_alloc) stops the loop and is returned as VOX_EIO, and a worker
+// thread that cannot be started leaves its share to the ones that did
+// (down to the calling thread alone).
 template <typename F>
-void parallel_for(int n, int threads, F&& body) {
+int parallel_for(int n, int threads, F&& body) noexcept {
   threads = std::max(1, std::min(threads, n));
   std::atomic<int> next{0};
-  auto work = [&]() {
-    for (int i; (i = next.fetch_add(1)) < n;) body(i);
+  std::atomic<bool> threw{false};
+  auto work = [&]() noexcept {
+    try {
+      for (int i; (i = next.fetch_add(1)) < n;) body(i);
+    } catch (...) {
+      threw.store(true);
+      next.store(n);
+    }
   };
   std::vector<std::thread> pool;
-  for (int k = 1; k < threads; ++k) pool.emplace_back(work);
+  try {
+    pool.reserve(threads - 1);
+    for (int k = 1; k < threads; ++k) pool.emplace_back(work);
+  } catch (...) {
+    // std::system_error / bad_alloc: run with the workers already started
+  }
   work();
   for (auto& t : pool) t.join();
+  if (threw.load()) {
+    try {
+      return kfail(VOX_EIO, "host worker failed (out of memory?)");
+    } catch (...) {
+      return VOX_EIO;
+    }
+  }
+  return VOX_OK;
 }
 
 // header only (no payload read): rows / cols of the matrix at path:offset
@@ -380,14 +404,14 @@ extern "C" int vox_mat_shapes(const char* const* paths, const int64_t* offsets, 
                               int* cols, int threads) {
   if (n < 0 || (n > 0 && (!paths || !offsets || !rows || !cols))) return kfail(VOX_EINVAL, "null argument");
   FirstError err;
-  parallel_for(n, threads, [&](int i) {
+  const int prc = parallel_for(n, threads, [&](int i) {
     if (err.code.load()) return;
     const int rc = paths[i] ? read_shape_at(paths[i], offsets[i], &rows[i], &cols[i])
                             : kfail(VOX_EINVAL, "null path");
     if (rc) err.set(rc, (std::string(paths[i] ? paths[i] : "?") + ": " + vox_last_error()).c_str());
   });
   if (err.code.load()) return kfail(err.code.load(), err.msg.c_str());
-  return VOX_OK;
+  return prc;
 }
 
 extern "C" int vox_read_chunks(const char* const* paths, const int64_t* offsets, const int* r0,
@@ -396,7 +420,7 @@ extern "C" int vox_read_chunks(const char* const* paths, const int64_t* offsets,
   if (n < 0 || f <= 0 || len <= 0 || (n > 0 && (!paths || !offsets || !r0 || !T || !c0 || !start || !out)))
     return kfail(VOX_EINVAL, "bad arguments");
   FirstError err;
-  parallel_for(n, threads, [&](int i) {
+  const int prc = parallel_for(n, threads, [&](int i) {
     if (err.code.load()) return;
     auto bad = [&](int rc) {
       err.set(rc, (std::string(paths[i] ? paths[i] : "?") + ": " + vox_last_error()).c_str());
@@ -428,5 +452,5 @@ extern "C" int vox_read_chunks(const char* const* paths, const int64_t* offsets,
       std::memcpy(o, u + (size_t)start[i] * f, (size_t)len * f * 4);
   });
   if (err.code.load()) return kfail(err.code.load(), err.msg.c_str());
-  return VOX_OK;
+  return prc;
 }

@@ -23,7 +23,12 @@ enum DType { F32 = 0, BF16 = 1 };
 //   RES       v += res[p][c]              (residual, res2net_model.py:100), only c < ysplit
 //   RELU      v = max(v,0)
 //   PARTIAL   raw accumulator -> split-K slab (no other flag applies)
-enum EpiFlags { EPI_PRE_RELU = 1, EPI_AFFINE = 2, EPI_RES = 4, EPI_RELU = 8, EPI_PARTIAL = 16 };
+// EPI_BN2D: TF1's non-fused inference BN of the 2-D head (tf.nn.batch_normalization,
+// what tf.compat.v1.layers picks for a 2-D input): x * inv + (-mean * inv), the
+// `mean` table holding -mean * inv (bn2d below); EPI_AFFINE is the fused form
+// (x - mean) * inv of the 4-D BNs
+enum EpiFlags { EPI_PRE_RELU = 1, EPI_AFFINE = 2, EPI_RES = 4, EPI_RELU = 8, EPI_PARTIAL = 16,
+                EPI_BN2D = 32 };
 
 // NHWC implicit-GEMM convolution, C[cout][pixel] = W[cout][k] * im2col[k][pixel].
 struct ConvParams {

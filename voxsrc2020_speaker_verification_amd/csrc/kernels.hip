@@ -1431,6 +1431,7 @@ __global__ __launch_bounds__(256) void splitk_reduce(const float* __restrict__ p
   for (; z < S; ++z) v += src[(size_t)z * zs];
   if (flags & EPI_PRE_RELU) v = fmaxf(v, 0.f);
   if (flags & EPI_AFFINE) v = (v - mean[c]) * inv[c];
+  if (flags & EPI_BN2D) v = bn2d(v, inv[c], mean[c]);
   if (flags & EPI_RELU) v = fmaxf(v, 0.f);
   out[(size_t)pix * ldo + c] = v;
 }
@@ -1581,8 +1582,8 @@ __global__ __launch_bounds__(64 * TS, PRO ? 4 : 1) void stats_pool_k(const T* __
       float m = mu[e];
       const int fm = w * 2 * C + ch * VN + e, fs = fm + C;
       if (mean) {
-        m = (m - mean[fm]) * inv[fm];
-        sd = (sd - mean[fs]) * inv[fs];
+        m = bn2d(m, inv[fm], mean[fm]);
+        sd = bn2d(sd, inv[fs], mean[fs]);
       }
       o[e] = m;
       o[C + e] = sd;
@@ -1673,8 +1674,8 @@ __global__ __launch_bounds__(256) void stats_pool_col(const bf16_t* __restrict__
     float m = mu[e];
     const int fm = w * 2 * C + ch * VN + e, fs = fm + C;
     if (mean) {
-      m = (m - mean[fm]) * inv[fm];
-      sd = (sd - mean[fs]) * inv[fs];
+      m = bn2d(m, inv[fm], mean[fm]);
+      sd = bn2d(sd, inv[fs], mean[fs]);
     }
     om[e] = m;
     os[e] = sd;
@@ -1976,8 +1977,8 @@ __global__ void att_pool_k(const T* __restrict__ x, const float* __restrict__ lg
   const float sd = sqrtf(wss - wm * wm + eps);
   float* o = out + n * W * 2 * C + (int64_t)w * 2 * C;
   const int j0 = w * 2 * C + c, j1 = j0 + C;
-  o[c] = mean ? (wm - mean[j0]) * inv[j0] : wm;
-  o[C + c] = mean ? (sd - mean[j1]) * inv[j1] : sd;
+  o[c] = mean ? bn2d(wm, inv[j0], mean[j0]) : wm;
+  o[C + c] = mean ? bn2d(sd, inv[j1], mean[j1]) : sd;
 }
 
 hipError_t launch_att_pool(DType t, const void* x, const float* lg, int N, int H, int W, int C,

@@ -205,7 +205,8 @@ def main(argv=None):
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--cohort-spk2utt", default=None)
     ap.add_argument("--lanes", type=int, default=4,
-                    help="concurrent extraction handles / streams per GPU")
+                    help="concurrent extraction handles / streams per GPU (each its own "
+                         "weights + a workspace for the largest batch: see extract --help)")
     ap.add_argument("--reader-threads", type=int, default=None)
     ap.add_argument("--resume", action="store_true",
                     help="reuse per-rank xvector.<i>.ark/.scp that already hold the rank's shard")

@@ -98,7 +98,11 @@ def main(argv=None):
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--no-cmn", action="store_true", help="features are already CMN'd")
     ap.add_argument("--lanes", type=int, default=4,
-                    help="concurrent extraction handles / streams on the device")
+                    help="concurrent extraction handles / streams per GPU.  Each lane is a "
+                         "full handle with its own copy of the weights and a workspace sized "
+                         "for the largest batch (--batch x 1000 frames: ~5.6 GB for res2net50 at "
+                         "--batch 64), so device memory grows with the lane count.  The lanes' "
+                         "streams and pinned buffers come from PyTorch (ROCm build)")
     ap.add_argument("--reader-threads", type=int, default=None,
                     help="host threads decoding + CMN'ing features (default: usable CPUs, <= 16)")
     a = ap.parse_args(argv)

@@ -271,6 +271,12 @@ class LanePool:
             stop.append(1)
             for t in lanes:
                 t.join()
+            # a lane that stopped early (its own error, a peer's, or the caller
+            # abandoning the generator) may have left its last batch queued: the
+            # H2D from its pinned buffer, the forward and the D2H still run on
+            # its stream.  Drain them before the buffers can be freed or reused
+            for s in self.streams:
+                s.synchronize()
         if err is not None:
             raise err
 
