@@ -76,6 +76,22 @@ int vox_embed(vox_model* m, const float* x, int n, int t, int f, float* out);
  * explicit stream, or synchronise, when the inputs were produced there). */
 int vox_embed_device(vox_model* m, const float* d_x, int n, int t, int f,
                      float* d_out, void* stream);
+/* Ragged batches: utterance i of the [n,t,f] batch holds lens[i] frames
+ * (1 <= lens[i] <= t), its rows past them are padding (any values).  Each
+ * embedding equals the one vox_embed computes for that utterance alone at
+ * t = lens[i] (the same per-utterance chunk as tf_extract.py:108 runs), bit for
+ * bit: every kernel that reads a row's neighbours treats the padded rows as
+ * the SAME / fixed padding of an utterance that ends at lens[i], and the stats
+ * pool averages its lens[i] (downsampled) rows.  So chunks of different
+ * lengths share one batch and one resident plan keyed on (n, t) -- what the
+ * streaming extractor buckets real length distributions into.  res2net models
+ * without attentive pooling in VOX_BF16; other plans return VOX_EINVAL.
+ * _device: d_lens is a device int32 [n] array (read in stream order);
+ * vox_embed_lens: host buffers, lens checked on the host. */
+int vox_embed_device_lens(vox_model* m, const float* d_x, int n, int t, int f,
+                          const int* d_lens, float* d_out, void* stream);
+int vox_embed_lens(vox_model* m, const float* x, int n, int t, int f, const int* lens,
+                   float* out);
 /* One utterance of any length t >= 25, chunked at 1000 frames. */
 int vox_embed_utt(vox_model* m, const float* x, int t, int f, float* out);
 

@@ -57,6 +57,9 @@ _SIGS = [
     ("vox_embed", C.c_int, [_P, _F, C.c_int, C.c_int, C.c_int, _F]),
     ("vox_embed_device", C.c_int, [_P, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, _P]),
     ("vox_embed_utt", C.c_int, [_P, _F, C.c_int, C.c_int, _F]),
+    ("vox_embed_device_lens", C.c_int,
+     [_P, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, _P]),
+    ("vox_embed_lens", C.c_int, [_P, _F, C.c_int, C.c_int, C.c_int, C.c_void_p, _F]),
     ("vox_profile", C.c_int, [_P, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, _F,
                               C.POINTER(C.c_double), C.POINTER(C.c_double),
                               C.POINTER(C.c_int), C.c_int, _P]),

@@ -197,10 +197,12 @@ struct Op {
   const float* in_mean = nullptr;  // type 2: input BN+ReLU fused into the pool (DPN68)
   const float* in_inv = nullptr;
   int cin = 0;
+  // ragged batches (types 11, 2, 3): per-utterance frames + this op's shift
+  const int* vlen = nullptr; int vsh = 0;
   double flops = 0, bytes = 0;
 };
 
-enum Slot { S_IN, S_X0, S_X1, S_A, S_B, S_SC, S_POOL, S_PART, S_NSLOTS };
+enum Slot { S_IN, S_X0, S_X1, S_A, S_B, S_SC, S_POOL, S_PART, S_LEN, S_NSLOTS };
 
 // A layer output the plan exposes for layer-by-layer checks (vox_debug_taps):
 // after ops [0, op_end) have run, `p` holds that layer's NHWC output.
@@ -214,6 +216,7 @@ struct Tap {
 // captured graph, keyed by the shape and the device pointers it was built for.
 struct PlanEntry {
   int n = -1, t = -1;
+  bool rag = false;     // ragged-batch plan (vox_embed_device_lens)
   const float* x = nullptr;
   float* out = nullptr;
   std::vector<Op> plan;
@@ -240,6 +243,7 @@ struct vox_model {
   hipStream_t stream = nullptr;
   // plan cache
   int plan_n = -1, plan_t = -1;
+  bool plan_rag = false;       // built for per-utterance lengths (S_LEN holds them)
   const float* plan_x = nullptr;
   float* plan_out = nullptr;
   std::vector<Op> plan;
@@ -266,7 +270,7 @@ struct vox_model {
   int graph_after = 1;
   uint64_t clock = 0;
   int64_t plans_built = 0, plan_hits = 0, plans_dropped = 0;
-  DevBuf stage_in, stage_out;  // host-API staging
+  DevBuf stage_in, stage_out, stage_len;  // host-API staging
   float eps4 = 1.001e-5f, eps2 = 1e-5f;  // BN epsilons (blob header may override)
   // Plan switches: kernel-routing A/B and parity knobs, 0 = the product plan.
   // Read once at load from the environment through kPlanEnv (below); each
@@ -682,6 +686,10 @@ struct Builder {
   vox_model* m;
   bool dry;
   std::vector<Op>* ops;
+  // ragged batches: the device frame counts every row-aware kernel reads, and
+  // the downsampling shift of the rows the ops being emitted read
+  const int* vlen = nullptr;
+  int vsh = 0;
   char* base(Slot s, size_t bytes) {
     m->slot_need[s] = std::max(m->slot_need[s], bytes);
     return dry ? nullptr : (char*)m->slots[s].p;
@@ -725,6 +733,7 @@ static void emit_conv(Builder& B, const ConvW& cw, Act x, const void* x2, int ld
   // handful of tiles), so an utterance's embedding bits do not depend on its
   // batch (tf_extract.py:27 extracts every utterance on its own)
   p.any_m = B.m->family == "tdnn" ? 1 : 0;
+  p.vlen = B.vlen; p.vsh = B.vsh;
   p.fast4 = (cw.cout % 4 == 0 && ldy % 4 == 0 && (ysplit >= (1 << 30) || (ysplit % 4 == 0 && ldy2 % 4 == 0)) &&
              (!res || ldr % 4 == 0) && cw.groups == 1) ? 1 : 0;
   op.cl.wco = cw.wco;
@@ -903,6 +912,7 @@ static void emit_pool(Builder& B, Act x, float* out, const BNW& bn, const BNW* i
   Op op;
   op.kind = OP_POOL;
   op.type = 2;
+  op.vlen = B.vlen; op.vsh = B.vsh;
   op.src = x.p; op.N = x.N; op.H = x.H; op.W = x.W; op.C = x.C;
   op.mean = (const float*)bn.mean->p;
   op.inv = (const float*)bn.inv->p;
@@ -1039,6 +1049,7 @@ static void emit_stem(Builder& B, const ConvW& stem, const float* x, int n, int 
     op.kind = OP_CONV;
     op.type = 11;
     op.src = x; op.dst = y; op.N = n; op.H = H; op.W = W; op.C = stem.cout;
+    op.vlen = B.vlen; op.vsh = B.vsh;
     op.part = (const float*)stem.wstem->p;
     op.mean = (const float*)stem.mean->p;
     op.inv = (const float*)stem.inv->p;
@@ -1156,6 +1167,7 @@ static int build_res2net(Builder& B, const float* x, int n, int t, float* out) {
             q.wp = pr.wpair->p; q.mp = (const float*)pr.mean->p; q.ip = (const float*)pr.inv->p;
           }
           q.dbg = m->bneck_dbg;
+          q.vlen = B.vlen; q.vsh = B.vsh;
           Op op;
           op.kind = OP_CONV;
           op.type = 12;
@@ -1211,6 +1223,7 @@ static int build_res2net(Builder& B, const float* x, int n, int t, float* out) {
           }
           q.lds = s2_fused_lds(cur.C, w, s, W);
           q.dbg = m->bneck_dbg;
+          q.vlen = B.vlen; q.vsh = B.vsh;
           Op op;
           op.kind = OP_CONV;
           op.type = 22;
@@ -1249,6 +1262,7 @@ static int build_res2net(Builder& B, const float* x, int n, int t, float* out) {
           }
           q.lds = chain_fused_lds(cur.C, w, s, W);
           q.dbg = m->bneck_dbg;
+          q.vlen = B.vlen; q.vsh = B.vsh;
           Op op;
           op.kind = OP_CONV;
           op.type = 24;
@@ -1294,6 +1308,7 @@ static int build_res2net(Builder& B, const float* x, int n, int t, float* out) {
             fl += 2.0 * n * H * W * 9.0 * w * w;
           }
           q.lds = chain_rows_lds(w, s, W);
+          q.vlen = B.vlen; q.vsh = B.vsh;
           Op op;
           op.kind = OP_CONV;
           op.type = 13;
@@ -1377,6 +1392,7 @@ static int build_res2net(Builder& B, const float* x, int n, int t, float* out) {
             q.inv[j] = (const float*)br.inv->p;
           }
           q.lds = split_s2_lds(w, s, W);
+          q.vlen = B.vlen; q.vsh = B.vsh;
           Op op;
           op.kind = OP_CONV;
           op.type = 14;
@@ -1412,6 +1428,7 @@ static int build_res2net(Builder& B, const float* x, int n, int t, float* out) {
           p.Cout = br.cout; p.coutp = br.coutp;
           p.kh = br.kh; p.kw = br.kw; p.sh = p.sw = stride; p.dh = p.dw = 1; p.ph = p.pw = 1;
           p.groups = br.groups; p.flags = EPI_AFFINE | EPI_RELU;
+          p.vlen = B.vlen; p.vsh = B.vsh;
           ok = br.wtc && br.mean && br.cin == w && br.cout == w && conv3_pipe_ok(p);
           // stride-1 w = 96: K-split register weights, 32x32 MFMA tiles (conv3k.hip),
           // or one 16-cout tile per wave (conv3r.hip, VOXEMB_NO_CONV3_KS)
@@ -1449,6 +1466,7 @@ static int build_res2net(Builder& B, const float* x, int n, int t, float* out) {
         op.lds = sw; op.N = n; op.H = H; op.W = W; op.C = w;
         op.dst = Bc ? Bc + (size_t)(s - 1) * w * es : nullptr;
         op.ldd = sw; op.Ho = Ho; op.Wo = Wo;
+        op.vlen = B.vlen; op.vsh = B.vsh;
         op.bytes = (double)es * ((double)n * H * W * w + (double)n * Ho * Wo * w);
         B.ops->push_back(op);
       }
@@ -1460,6 +1478,7 @@ static int build_res2net(Builder& B, const float* x, int n, int t, float* out) {
       cur = Act{yo, c1c.cout, n, Ho, Wo, c1c.cout};
       B.tap(yo, n, Ho, Wo, c1c.cout, c1c.cout);
       std::swap(cur_s, nxt_s);
+      if (stride == 2) ++B.vsh;   // the next blocks read rows at the halved resolution
       H = Ho;
       W = Wo;
     }
@@ -1720,7 +1739,7 @@ static void stash_current(vox_model* m) {
     m->cache.erase(m->cache.begin() + (long)lru);
   }
   PlanEntry e;
-  e.n = m->plan_n; e.t = m->plan_t; e.x = m->plan_x; e.out = m->plan_out;
+  e.n = m->plan_n; e.t = m->plan_t; e.x = m->plan_x; e.out = m->plan_out; e.rag = m->plan_rag;
   e.plan.swap(m->plan);
   e.taps.swap(m->taps);
   e.exec = m->graph_exec;
@@ -1731,11 +1750,35 @@ static void stash_current(vox_model* m) {
   m->cache.push_back(std::move(e));
 }
 
-static int build_plan(vox_model* m, const float* x, int n, int t, float* out) {
+// Ops whose kernels honour per-utterance lengths (ragged batches): every
+// kernel that reads a row's neighbours masks the rows past the utterance's
+// (device_common.h valid_rows); the 1x1 GEMMs and the head are per pixel.
+static bool ragged_ok(const Op& op, DType dt) {
+  if (dt != BF16) return false;
+  switch (op.type) {
+    case 11: return op.C == 32;                    // stem_conv1_c32
+    case 12: case 13: case 14: case 22: case 24:   // bneck / chain / stride-2 row kernels
+    case 20: case 26: case 28: case 30:            // 3x3 branch kernels
+    case 1: case 2: case 4:                        // split-K reduce, stats pool, input cast
+      return true;
+    case 3: return op.C % 8 == 0 && op.lds % 8 == 0 && op.ldd % 8 == 0;   // avgpool3s2_v8
+    case 5: return op.kind == OP_HEAD;             // the fp32 head dense
+    case 21: case 9: case 18: case 29: case 8:     // 1x1 convs (per pixel)
+      return op.cp.kh == 1 && op.cp.kw == 1 && !op.cp.in_mean;
+  }
+  return false;
+}
+
+static int build_plan(vox_model* m, const float* x, int n, int t, float* out, bool rag = false) {
   auto run = [&](bool dry) -> int {
     Builder B{m, dry, &m->plan};
     m->plan.clear();
     m->taps.clear();
+    if (rag) {
+      if (m->family != "res2net" || m->att)
+        return fail(VOX_EINVAL, "per-utterance lengths: res2net models without attentive pooling only");
+      B.vlen = (const int*)B.base(S_LEN, (size_t)n * 4);
+    }
     if (m->family == "tdnn") return build_tdnn(B, x, n, t, out);
     if (m->family == "res2net") return build_res2net(B, x, n, t, out);
     if (m->family == "dpn") return build_dpn(B, x, n, t, out);
@@ -1770,8 +1813,17 @@ static int build_plan(vox_model* m, const float* x, int n, int t, float* out) {
   if (grew) HIPCHK(hipStreamSynchronize(m->stream));
   rc = run(false);
   if (rc) return rc;
+  if (rag)
+    for (const Op& op : m->plan)
+      if (!ragged_ok(op, m->dt)) {
+        m->plan.clear();
+        m->taps.clear();
+        return fail(VOX_EINVAL, "per-utterance lengths: op type " + std::to_string(op.type) +
+                                    " of this model's plan does not mask padded rows");
+      }
   m->plan_n = n;
   m->plan_t = t;
+  m->plan_rag = rag;
   m->plan_x = x;
   m->plan_out = out;
   m->plan_uses = 0;
@@ -1810,17 +1862,17 @@ static hipError_t run_op(vox_model* m, const Op& op, hipStream_t s) {
                              op.inv, op.out, s);
     case 11:
       return launch_stem(m->dt, (const float*)op.src, op.N, op.H, op.W, op.part, op.C, op.mean,
-                         op.inv, op.dst, s);
+                         op.inv, op.dst, s, op.vlen);
     case 5: return launch_conv(F32, op.cp, op.cl, s);
     case 1:
       return launch_splitk_reduce(op.part, op.S, op.M, op.coutp, op.cout, op.mean, op.inv,
                                   op.flags, op.out, op.ldo, s);
     case 2:
       return launch_stats_pool(m->dt, op.src, op.N, op.H, op.W, op.C, op.mean, op.inv, op.out, s,
-                               op.in_mean, op.in_inv);
+                               op.in_mean, op.in_inv, op.vlen, op.vsh);
     case 3:
       return launch_avgpool3s2(m->dt, op.src, op.lds, op.N, op.H, op.W, op.C, op.dst, op.ldd, op.Ho,
-                               op.Wo, s);
+                               op.Wo, s, op.vlen, op.vsh);
     case 4: return launch_convert_f32(m->dt, (const float*)op.src, op.dst, op.count, s);
     case 6:
       return launch_bnrelu_inplace(m->dt, op.dst, op.ldd, (int64_t)op.N * op.H * op.W, op.C,
@@ -1837,13 +1889,16 @@ static int check_shape(vox_model* m, int n, int t, int f) {
   return VOX_OK;
 }
 
-static int ensure_plan(vox_model* m, const float* d_x, int n, int t, float* d_out) {
-  if (m->plan_n == n && m->plan_t == t && m->plan_x == d_x && m->plan_out == d_out) return VOX_OK;
+static int ensure_plan(vox_model* m, const float* d_x, int n, int t, float* d_out, bool rag = false) {
+  if (m->plan_n == n && m->plan_t == t && m->plan_x == d_x && m->plan_out == d_out &&
+      m->plan_rag == rag)
+    return VOX_OK;
   for (PlanEntry& e : m->cache) {
-    if (e.n != n || e.t != t || e.x != d_x || e.out != d_out) continue;
+    if (e.n != n || e.t != t || e.x != d_x || e.out != d_out || e.rag != rag) continue;
     // swap the resident plan in; the current one takes its cache entry
     std::swap(e.n, m->plan_n);
     std::swap(e.t, m->plan_t);
+    std::swap(e.rag, m->plan_rag);
     std::swap(e.x, m->plan_x);
     std::swap(e.out, m->plan_out);
     e.plan.swap(m->plan);
@@ -1858,7 +1913,7 @@ static int ensure_plan(vox_model* m, const float* d_x, int n, int t, float* d_ou
     ++m->plan_hits;
     return VOX_OK;
   }
-  return build_plan(m, d_x, n, t, d_out);
+  return build_plan(m, d_x, n, t, d_out, rag);
 }
 
 // ------------------------------------------------------------------ C-ABI
@@ -1949,13 +2004,15 @@ extern "C" int vox_precision(const vox_model* m) {
   return m ? (m->dt == BF16 ? VOX_BF16 : VOX_FP32) : VOX_EINVAL;
 }
 
-extern "C" int vox_embed_device(vox_model* m, const float* d_x, int n, int t, int f, float* d_out,
-                                void* stream) {
+// d_lens (device int32 [n], each in [1, t]) or null: a ragged batch -- utterance
+// i holds d_lens[i] frames padded to t; its embedding equals the unpadded run's
+static int embed_device(vox_model* m, const float* d_x, int n, int t, int f, const int* d_lens,
+                        float* d_out, void* stream) {
   if (!m || !d_x || !d_out) return fail(VOX_EINVAL, "null argument");
   int rc = check_shape(m, n, t, f);
   if (rc) return rc;
   HIPCHK(hipSetDevice(m->device));
-  if ((rc = ensure_plan(m, d_x, n, t, d_out))) return rc;
+  if ((rc = ensure_plan(m, d_x, n, t, d_out, d_lens != nullptr))) return rc;
   hipStream_t s = stream ? (hipStream_t)stream : m->stream;
   if (m->use_graph && !m->graph_exec && m->plan_uses >= m->graph_after) {
     // capture on the handle's own stream (the caller's may be the legacy null
@@ -1978,6 +2035,8 @@ extern "C" int vox_embed_device(vox_model* m, const float* d_x, int n, int t, in
   }
   // calls on different streams share the slots: order after the previous launch
   HIPCHK(hipStreamWaitEvent(s, m->done, 0));
+  // this call's frame counts into the slot the plan's kernels read (stream-ordered)
+  if (d_lens) HIPCHK(hipMemcpyAsync(m->slots[S_LEN].p, d_lens, (size_t)n * 4, hipMemcpyDeviceToDevice, s));
   if (m->use_graph && m->graph_exec) {
     HIPCHK(hipGraphLaunch(m->graph_exec, s));
   } else {
@@ -1985,6 +2044,41 @@ extern "C" int vox_embed_device(vox_model* m, const float* d_x, int n, int t, in
   }
   HIPCHK(hipEventRecord(m->done, s));
   ++m->plan_uses;
+  return VOX_OK;
+}
+
+extern "C" int vox_embed_device(vox_model* m, const float* d_x, int n, int t, int f, float* d_out,
+                                void* stream) {
+  return embed_device(m, d_x, n, t, f, nullptr, d_out, stream);
+}
+
+extern "C" int vox_embed_device_lens(vox_model* m, const float* d_x, int n, int t, int f,
+                                     const int* d_lens, float* d_out, void* stream) {
+  if (!d_lens) return fail(VOX_EINVAL, "null lengths");
+  return embed_device(m, d_x, n, t, f, d_lens, d_out, stream);
+}
+
+extern "C" int vox_embed_lens(vox_model* m, const float* x, int n, int t, int f, const int* lens,
+                              float* out) {
+  if (!m || !x || !lens || !out) return fail(VOX_EINVAL, "null argument");
+  int rc = check_shape(m, n, t, f);
+  if (rc) return rc;
+  for (int i = 0; i < n; ++i)
+    if (lens[i] < 1 || lens[i] > t)
+      return fail(VOX_EINVAL, "length " + std::to_string(lens[i]) + " of utterance " +
+                                  std::to_string(i) + " outside [1, " + std::to_string(t) + "]");
+  HIPCHK(hipSetDevice(m->device));
+  const size_t in_b = (size_t)n * t * f * 4, out_b = (size_t)n * m->out_dim * 4;
+  HIPCHK(m->stage_in.ensure(in_b));
+  HIPCHK(m->stage_out.ensure(out_b));
+  HIPCHK(m->stage_len.ensure((size_t)n * 4));
+  HIPCHK(hipMemcpyAsync(m->stage_in.p, x, in_b, hipMemcpyHostToDevice, m->stream));
+  HIPCHK(hipMemcpyAsync(m->stage_len.p, lens, (size_t)n * 4, hipMemcpyHostToDevice, m->stream));
+  rc = embed_device(m, (const float*)m->stage_in.p, n, t, f, (const int*)m->stage_len.p,
+                    (float*)m->stage_out.p, m->stream);
+  if (rc) return rc;
+  HIPCHK(hipMemcpyAsync(out, m->stage_out.p, out_b, hipMemcpyDeviceToHost, m->stream));
+  HIPCHK(hipStreamSynchronize(m->stream));
   return VOX_OK;
 }
 

@@ -108,6 +108,8 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
   const int n = blockIdx.x / q.nseg;
   const int h0 = (blockIdx.x - n * q.nseg) * q.seg;
   const int h1 = min(H, h0 + q.seg);
+  // ragged batch: rows at or past Hn are this utterance's padding (zeros in the rings)
+  const int Hn = valid_rows(q.vlen, q.vsh, n, H);
   char* rings = smem;
   char* inb = smem + K::RING_BYTES;
   unsigned short* ktl = reinterpret_cast<unsigned short*>(inb + K::IN_BYTES);
@@ -303,7 +305,7 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
     stamp(t, 0);
     // ---------------- phase 0: 1x1a (row a) | 1x1c (row c)
     if (is_a && !(VOX_DBG(q) & 1)) {
-      const bool inimg = a >= 0 && a < H;
+      const bool inimg = a >= 0 && a < Hn;
       const int ch = 32 * pq + 8 * g;
       const int p = ch / WID, off = ch - p * WID;
       int sl = K::ZB(1) + (a & 3);                   // plane 0 -> z_1 = x_1
@@ -468,7 +470,7 @@ __global__ __launch_bounds__(512) void bneck_fused(BneckParams q) {
       const int k = ck;
       const int co = 16 * ci + 4 * g;
       const int r = a - 2 * k + 1;
-      const bool inimg = r >= 0 && r < H;
+      const bool inimg = r >= 0 && r < Hn;
       // ring geometry of stage k (wave-uniform -> scalar registers); tap row dy
       // of output row r is ring row (r - 1 + dy) & 3 of z_k
       const char* zring = rings + K::ZB(k) * ROWB;
@@ -636,6 +638,7 @@ __global__ __launch_bounds__((ChainRowsCfg<WID, S, PT>::NT)) void chain_rows(Cha
   const int n = blockIdx.x / nseg;
   const int h0 = (blockIdx.x - n * nseg) * q.R;
   const int h1 = min(H, h0 + q.R);
+  const int Hn = valid_rows(q.vlen, q.vsh, n, H);   // ragged batch (device_common.h)
   char* rings = smem;
   float* bmb = reinterpret_cast<float*>(smem + K::RING_BYTES);
   float* bib = bmb + (S - 1) * 16 * WCO;
@@ -690,7 +693,7 @@ __global__ __launch_bounds__((ChainRowsCfg<WID, S, PT>::NT)) void chain_rows(Cha
       const int c = tid + i * NT;
       const int px = c / K::CU, u = c - px * K::CU;
       xr[i] = make_uint4(0, 0, 0, 0);
-      if (c < 16 * PT * K::CU && px < W && r >= 0 && r < H)
+      if (c < 16 * PT * K::CU && px < W && r >= 0 && r < Hn)
         xr[i] = *reinterpret_cast<const uint4*>(A + (img + (size_t)r * W + px) * q.lda + u * 8);
     }
   };
@@ -722,7 +725,7 @@ __global__ __launch_bounds__((ChainRowsCfg<WID, S, PT>::NT)) void chain_rows(Cha
       const int k = ck;
       const int co = 16 * ci + 4 * g;
       const int r = a - 2 * k + 1;
-      const bool inimg = r >= 0 && r < H;
+      const bool inimg = r >= 0 && r < Hn;
       const int zd = k == 1 ? 3 : 4;
       const int zbase = k == 1 ? 0 : 3 + 4 * (k - 2);
       const int rb0 = __builtin_amdgcn_readfirstlane((zbase + (r - 1 + 840) % zd) * ROWB);
@@ -853,6 +856,7 @@ __global__ __launch_bounds__((ChainFusedCfg<CI, WID, S, PT>::NT)) void chain_fus
   const int n = blockIdx.x / nseg;
   const int h0 = (blockIdx.x - n * nseg) * q.R;
   const int h1 = min(H, h0 + q.R);
+  const int Hn = valid_rows(q.vlen, q.vsh, n, H);   // ragged batch (device_common.h)
   char* rings = smem;
   char* inb = smem + K::RING_BYTES;
   unsigned short* ktl = reinterpret_cast<unsigned short*>(inb + K::INB);
@@ -958,7 +962,7 @@ __global__ __launch_bounds__((ChainFusedCfg<CI, WID, S, PT>::NT)) void chain_fus
     {
       const int ch = 32 * (t16 >> 1) + 8 * g + 4 * (t16 & 1);
       const int p = ch / WID, off = ch - p * WID;
-      const bool inimg = a >= 0 && a < H;
+      const bool inimg = a >= 0 && a < Hn;
       int sl = (a + 840) & 3;                                   // plane 0 -> z_1
 #pragma unroll
       for (int d = 2; d < S; ++d)
@@ -1030,7 +1034,7 @@ __global__ __launch_bounds__((ChainFusedCfg<CI, WID, S, PT>::NT)) void chain_fus
       const int k = ck;
       const int co = 16 * ci + 4 * g;
       const int r = a - 2 * k + 1;
-      const bool inimg = r >= 0 && r < H;
+      const bool inimg = r >= 0 && r < Hn;
       // z_k ring (4 rows): tap row dy of output row r is ring row (r - 1 + dy) & 3
       const char* zring = rings + 4 * (k - 1) * ROWB;
       const int rbase = __builtin_amdgcn_readfirstlane(((r - 1 + 840) & 3) * ROWB);
@@ -1198,6 +1202,7 @@ __global__ __launch_bounds__((SplitS2Cfg<WID, S, WIN>::NT)) void split_s2_rows(C
   const int n = blockIdx.x / nseg;
   const int g0 = (blockIdx.x - n * nseg) * q.R;
   const int g1 = min(Ho, g0 + q.R);
+  const int Hn = valid_rows(q.vlen, q.vsh, n, H);   // ragged batch: input rows past it are padding
   char* rings = smem;
   const int ring_bytes = S * PLANEB;
   float* bmb = reinterpret_cast<float*>(smem + ring_bytes);
@@ -1263,7 +1268,7 @@ __global__ __launch_bounds__((SplitS2Cfg<WID, S, WIN>::NT)) void split_s2_rows(C
       const int px = cc / CU, u = cc - px * CU;
       const int r = r0 + rr;
       xr[i] = make_uint4(0, 0, 0, 0);
-      if (rr < 2 && r >= 0 && r < H)
+      if (rr < 2 && r >= 0 && r < Hn)
         xr[i] = *reinterpret_cast<const uint4*>(base + (rr * W + px) * lda + u * 8);
     }
   };
@@ -1439,6 +1444,7 @@ __global__ __launch_bounds__((S2FusedCfg<CI, WID, S, WIN>::NT)) void s2_fused(Ch
   const int n = blockIdx.x / nseg;
   const int g0 = (blockIdx.x - n * nseg) * q.R;
   const int g1 = min(Ho, g0 + q.R);
+  const int Hn = valid_rows(q.vlen, q.vsh, n, H);   // ragged batch: input rows past it are padding
   char* rings = smem;
   char* inb = smem + K::RING;
   float* bmb = reinterpret_cast<float*>(inb + 2 * K::INROW);
@@ -1582,7 +1588,7 @@ __global__ __launch_bounds__((S2FusedCfg<CI, WID, S, WIN>::NT)) void s2_fused(Ch
 #pragma unroll
         for (int s = 0; s < K::KSA; ++s) a0 = mfma_step(w1[s], bc[s], a0);
         const int r = 2 * ho + rr;
-        const bool inimg = r >= 0 && r < H;
+        const bool inimg = r >= 0 && r < Hn;
         char* dst = rings + p * PLANEB + ((r + 840) % 3) * ROWB + off * 2;
         const int px = 16 * j + col;
         bf16x4 o;

@@ -132,7 +132,7 @@ void conv3x3_pipe(ConvParams p) {
 
   const bf16_t* pa[C3_NA];
   const bf16_t* pb[C3_NB];
-  int hin[C3_NB], win[C3_NB];
+  int hin[C3_NB], win[C3_NB], hl[C3_NB];   // hl: the pixel's utterance's valid input rows
   auto set_load_tile = [&](int tj) {
     const int lid = t_first + tj * t_step;
     const int co0 = (lid % cblocks) * C3_BN;
@@ -152,6 +152,7 @@ void conv3x3_pipe(ConvParams p) {
       const int ho = rr / p.Wo, wo = rr - ho * p.Wo;
       hin[i] = ho * p.sh;
       win[i] = wo * p.sw;
+      hl[i] = valid_rows(p.vlen, p.vsh, n, p.H);   // ragged batch: rows past it are padding
       pb[i] = X + (((size_t)n * p.H + hin[i]) * p.W + win[i]) * p.ldx;
     }
   };
@@ -169,7 +170,7 @@ void conv3x3_pipe(ConvParams p) {
     for (int i = 0; i < C3_NA; ++i) c3_glds16(kin ? pa[i] + l_k * 64 : zero, base + i * 8192u);
 #pragma unroll
     for (int i = 0; i < C3_NB; ++i) {
-      const bool ok = kin && (unsigned)(hin[i] + dy) < (unsigned)p.H &&
+      const bool ok = kin && (unsigned)(hin[i] + dy) < (unsigned)hl[i] &&
                       (unsigned)(win[i] + dx) < (unsigned)p.W;
       c3_glds16(ok ? pb[i] + off : zero, base + (C3_NA + i) * 8192u);
     }

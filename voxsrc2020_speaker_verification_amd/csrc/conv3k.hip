@@ -203,7 +203,9 @@ __global__ __launch_bounds__(KS_NT) void conv3x3_ks(ConvParams p) {
 
   // window piece q of tile tj into buffer b: units [64q, 64q + 64), unit u =
   // chunk u % 13 of slot u / 13 (chunk 12 = the pad unit)
-  auto issue_piece = [&](int n, int r0w, int b, int q) __attribute__((always_inline)) {
+  // hn: the utterance's valid rows (ragged batches; H otherwise): rows past
+  // them are its SAME padding
+  auto issue_piece = [&](int n, int r0w, int b, int q, int hn) __attribute__((always_inline)) {
     int u = lane;
     asm volatile("" : "+v"(u));
     u += 64 * q;
@@ -211,7 +213,7 @@ __global__ __launch_bounds__(KS_NT) void conv3x3_ks(ConvParams p) {
     const int rr = x / SW, sc = x - rr * SW;
     const int row = r0w + rr;
     const bf16_t* src = zero;
-    if (c < KS_NCH && sc > 0 && rr < K::RMAX && row >= 0 && row < H)
+    if (c < KS_NCH && sc > 0 && rr < K::RMAX && row >= 0 && row < hn)
       src = X + ((size_t)n * HW + row * W + (sc - 1)) * p.ldx + c * 8;
     ks_glds16(src, lds0 + (uint32_t)b * K::WBUF + (uint32_t)q * 1024u);
   };
@@ -219,7 +221,8 @@ __global__ __launch_bounds__(KS_NT) void conv3x3_ks(ConvParams p) {
     const int id = t_first + tj * t_step;
     const int n = id / tpu, t = id - n * tpu;
     const int r0w = (t * KS_TP) / W - 1;   // image row of window row 0
-    for (int q = wave; q < K::WPC; q += KS_NW) issue_piece(n, r0w, b, q);
+    const int hn = p.vlen ? valid_rows(p.vlen, p.vsh, n, H) : H;
+    for (int q = wave; q < K::WPC; q += KS_NW) issue_piece(n, r0w, b, q, hn);
   };
 
   // the tile's x_{k+1} pixel rows (192 B each) into LDS, linear
@@ -280,17 +283,18 @@ __global__ __launch_bounds__(KS_NT) void conv3x3_ks(ConvParams p) {
     // (issued together here they held every wave ~2-4k clk per tile before
     // its first MFMA; conv3x3_ks 990 -> 967 us per step); same issue order
     // relative to the x rows and stores
-    int n1 = 0, r0w1 = 0;
+    int n1 = 0, r0w1 = 0, hn1 = H;
     const bool more = tj + 1 < ntiles;
     if (more) {
       const int id1 = t_first + (tj + 1) * t_step;
       n1 = id1 / tpu;
       r0w1 = ((id1 - n1 * tpu) * KS_TP) / W - 1;
+      if (p.vlen) hn1 = valid_rows(p.vlen, p.vsh, n1, H);
     }
     auto fill = [&](int s) __attribute__((always_inline)) {
       if (more && s % 6 == 3) {
         const int q = wave + KS_NW * (s / 6);
-        if (q < K::WPC) issue_piece(n1, r0w1, b ^ 1, q);
+        if (q < K::WPC) issue_piece(n1, r0w1, b ^ 1, q, hn1);
       }
     };
     auto nofill = [](int) {};

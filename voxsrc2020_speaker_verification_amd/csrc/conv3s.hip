@@ -134,6 +134,8 @@ __global__ __launch_bounds__(CS_NT) void conv3x3_s2r(ConvParams p) {
     const int id = t_first + tj * t_step;
     const int n = id / tpu, t = id - n * tpu;
     const int r0 = 2 * t * TR - 1;             // input row of window row 0
+    // ragged batch: the utterance's input rows past hn are its fixed padding
+    const int hn = p.vlen ? valid_rows(p.vlen, p.vsh, n, H) : H;
 #pragma unroll
     for (int i = 0; i < (K::WPC + CS_NW - 1) / CS_NW; ++i) {
       const int q = wave + CS_NW * i;
@@ -148,7 +150,7 @@ __global__ __launch_bounds__(CS_NT) void conv3x3_s2r(ConvParams p) {
         const int icol = sc <= WO ? 2 * sc - 1 : 2 * (sc - WO - 1);
         const int row = r0 + wrow;
         const bf16_t* src = zero;
-        if (sp < CS_NCH / 2 && row >= 0 && row < H && icol >= 0 && icol < K::WI)
+        if (sp < CS_NCH / 2 && row >= 0 && row < hn && icol >= 0 && icol < K::WI)
           src = X + ((size_t)n * H * K::WI + (size_t)row * K::WI + icol) * p.ldx + c * 8;
         cs_glds16(src, lds0 + (uint32_t)b * K::BUF + (uint32_t)q * 1024u);
       }

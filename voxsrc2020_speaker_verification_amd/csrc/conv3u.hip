@@ -144,6 +144,7 @@ __global__ __launch_bounds__(CU_NT) void conv3x3_utt(ConvParams p) {
     const int r0 = band * R;
     const int rb = min(R, H - r0);                  // rows of this band
     const int npx = rb * W;
+    const int hn = p.vlen ? valid_rows(p.vlen, p.vsh, n, H) : H;   // ragged batch: padding past hn
     // ---- window of the band: rows r0-1 .. r0+rb (zero outside the image)
     for (int q = wave; q < K::WPC; q += CU_NW) {
       int u = lane;
@@ -154,7 +155,7 @@ __global__ __launch_bounds__(CU_NT) void conv3x3_utt(ConvParams p) {
       const int rr = slot / SW, cc = slot - rr * SW;
       const int r = r0 - 1 + rr, wc = cc - 1;
       const bf16_t* src = zero;
-      if (sp < CU_NCH / 2 && cc > 0 && rr <= rb + 1 && r >= 0 && r < H)
+      if (sp < CU_NCH / 2 && cc > 0 && rr <= rb + 1 && r >= 0 && r < hn)
         src = X + (((size_t)n * H + r) * W + wc) * p.ldx + c * 8;
       cu_glds16(src, lds0 + (uint32_t)q * 1024u);
     }

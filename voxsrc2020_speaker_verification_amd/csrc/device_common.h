@@ -9,6 +9,16 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// Ragged batches (vox_embed_device_lens): utterance n of a batch padded to H
+// rows holds vlen[n] frames.  At a layer downsampled by 2^vsh its valid rows are
+// ceil(vlen[n] / 2^vsh) -- every stride-2 layer (TF fixed padding / SAME, k = 3)
+// maps an input of h rows to ceil(h / 2) -- and a kernel reads the rows at or
+// past that as the zero padding of an utterance ending there, so a padded
+// utterance's valid outputs equal the unpadded run's.  vlen null: H.
+__device__ __forceinline__ int valid_rows(const int* vlen, int vsh, int n, int H) {
+  return vlen ? min(H, (vlen[n] + (1 << vsh) - 1) >> vsh) : H;
+}
+
 // TF1 nn.batch_normalization at inference (the 2-D head BNs, non-fused):
 // x * inv + (-mean * inv) as two roundings -- its Mul and Add graph ops --
 // never contracted to an FMA; nmi = -mean * inv is precomputed at load

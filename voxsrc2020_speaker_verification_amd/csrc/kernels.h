@@ -57,6 +57,9 @@ struct ConvParams {
   // gemm1x1_ws at any tile count (the plan fixes the route per model, not per
   // batch: the TDNN's bits must not depend on how many utterances share a batch)
   int any_m;
+  // ragged batches: per-utterance frame counts (device) and this layer's
+  // downsampling shift (device_common.h valid_rows); null = every row valid
+  const int* vlen; int vsh;
 };
 
 struct ConvLaunch {
@@ -84,6 +87,7 @@ struct ChainParams {
   const void* wa; const float* ma; const float* ia;
   int dbg;                          // diagnostics (VOXEMB_BNECK_DBG): skip parts, garbage out
                                     // (read only in VOX_DIAG builds, see VOX_DBG)
+  const int* vlen; int vsh;         // ragged batches (ConvParams::vlen); vsh of the input rows
 };
 hipError_t launch_split_chain(const ChainParams& q, int wco, int wpx, hipStream_t s);
 // Row-streamed split chain (bneck.hip): utterance segments of q.R rows, q.nwaves
@@ -126,6 +130,7 @@ struct BneckParams {
   const void* wp;                   // projection shortcut [C][Cin] paired rows (Cin != C)
   const float* mp; const float* ip;
   int dbg;                          // timing experiments only: skip parts (0 = normal)
+  const int* vlen; int vsh;         // ragged batches (ConvParams::vlen)
 };
 // LDS bytes of the instantiated shape, or -1 when (C, w, split, W) has none.
 int bneck_lds(int Cin, int C, int w, int split, int W);
@@ -185,7 +190,8 @@ hipError_t launch_conv3_pipe(const ConvParams& p, int num_cu, hipStream_t s);
 // 1-input-channel 3x3 SAME stem + BN + ReLU from the fp32 features;
 // wts = [9][Cout] fp32 (bf16-rounded values in bf16 mode), Cout <= 64.
 hipError_t launch_stem(DType t, const float* x, int N, int H, int W, const float* wts, int Cout,
-                       const float* mean, const float* inv, void* y, hipStream_t s);
+                       const float* mean, const float* inv, void* y, hipStream_t s,
+                       const int* vlen = nullptr);
 int conv_kstep(DType t);   // 32 (bf16) / 16 (fp32)
 // Attentive statistics pooling glue (fp32): bf16 -> fp32 copy; h = tanh(h +
 // b[n][w]) over [N][H][W][A]; softmax-over-time weighted mean/std (+ optional
@@ -266,12 +272,15 @@ hipError_t launch_splitk_reduce(const float* partial, int S, int M, int coutp, i
                                 float* out, int ldo, hipStream_t s);
 
 // in_mean / in_inv: optional input BN+ReLU (DPN68's concat_bn_relu) fused into the read
+// vlen / vsh (ragged batches): utterance n pools its valid_rows only
 hipError_t launch_stats_pool(DType t, const void* x, int N, int H, int W, int C,
                              const float* mean, const float* inv, float* out, hipStream_t s,
-                             const float* in_mean = nullptr, const float* in_inv = nullptr);
+                             const float* in_mean = nullptr, const float* in_inv = nullptr,
+                             const int* vlen = nullptr, int vsh = 0);
 
 hipError_t launch_avgpool3s2(DType t, const void* x, int ldx, int N, int H, int W, int C,
-                             void* y, int ldy, int Ho, int Wo, hipStream_t s);
+                             void* y, int ldy, int Ho, int Wo, hipStream_t s,
+                             const int* vlen = nullptr, int vsh = 0);
 
 hipError_t launch_convert_f32(DType t, const float* x, void* y, int64_t n, hipStream_t s);
 

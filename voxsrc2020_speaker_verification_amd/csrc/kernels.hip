@@ -1258,7 +1258,8 @@ __global__ __launch_bounds__(256) void stem_conv1_c32(const float* __restrict__ 
                                                      int W, const float* __restrict__ wts,
                                                      const float* __restrict__ mean,
                                                      const float* __restrict__ inv,
-                                                     bf16_t* __restrict__ y) {
+                                                     bf16_t* __restrict__ y,
+                                                     const int* __restrict__ vlen) {
   typedef float f32x2 __attribute__((ext_vector_type(2)));
   constexpr int COUT = 32, PP = STEM_PP;   // PP pixels per thread, 256 apart
   __shared__ __attribute__((aligned(16))) float sw[9 * COUT];
@@ -1281,10 +1282,12 @@ __global__ __launch_bounds__(256) void stem_conv1_c32(const float* __restrict__ 
     const int hi = (int)(hw / (unsigned)W);
     const int wi = (int)(hw - (unsigned)hi * (unsigned)W);
     const float* xi = x + (pix - (int64_t)hw);
+    // ragged batch: rows past the utterance's frames are its SAME padding
+    const int Hn = vlen ? valid_rows(vlen, 0, (int)((pix - (int64_t)hw) / ((int64_t)H * W)), H) : H;
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
       const int yy = hi + t / 3 - 1, xx = wi + t % 3 - 1;
-      const bool ok = yy >= 0 && yy < H && xx >= 0 && xx < W;
+      const bool ok = yy >= 0 && yy < Hn && xx >= 0 && xx < W;
       const int yc = min(max(yy, 0), H - 1), xc = min(max(xx, 0), W - 1);
       const float a = xi[yc * W + xc];
       v[u][t] = ok ? (float)(bf16_t)a : 0.f;
@@ -1341,16 +1344,18 @@ __global__ __launch_bounds__(256) void stem_conv1_c32(const float* __restrict__ 
 }
 
 hipError_t launch_stem(DType t, const float* x, int N, int H, int W, const float* wts, int Cout,
-                       const float* mean, const float* inv, void* y, hipStream_t s) {
+                       const float* mean, const float* inv, void* y, hipStream_t s,
+                       const int* vlen) {
   if (Cout > 64) return hipErrorInvalidValue;
   const int64_t n = (int64_t)N * H * W;
   const unsigned g = (unsigned)((n + 255) / 256);
   if (t == BF16 && Cout == 32) {
     hipLaunchKernelGGL(stem_conv1_c32, dim3((unsigned)((n + 256 * STEM_PP - 1) / (256 * STEM_PP))),
                        dim3(256), 0, s, x, N, H, W, wts, mean, inv,
-                       (bf16_t*)y);
+                       (bf16_t*)y, vlen);
     return hipGetLastError();
   }
+  if (vlen) return hipErrorInvalidValue;   // ragged batches: the c32 stem only
   if (t == BF16 && Cout == 10) {
     hipLaunchKernelGGL(stem_conv1_small<10>, dim3(g), dim3(256), 0, s, x, N, H, W, wts, mean, inv,
                        (bf16_t*)y);
@@ -1456,14 +1461,20 @@ hipError_t launch_splitk_reduce(const float* partial, int S, int M, int coutp, i
 // is read, rounded to T: the bits of DPN68's in-place concat_bn_relu pass
 // (bnrelu_k, dpn_model.py:24-29) followed by the pool, without the extra
 // read + write of the map.
-template <typename T, int VN, int TS, bool PRO = false>
+// RAG (ragged batches, vlen): utterance n pools its valid_rows Hn, in the
+// order the unpadded run (H = Hn) takes -- stats_pool_ts' slice count for Hn
+// (bf16 / 8 channels: the sequential stats_pool_col up to 32 rows) -- the
+// slices past it idle (their zero partials add exactly)
+template <typename T, int VN, int TS, bool PRO = false, bool RAG = false>
 __global__ __launch_bounds__(64 * TS, PRO ? 4 : 1) void stats_pool_k(const T* __restrict__ x, int N, int H,
                                                         int W, int C,
                                                         const float* __restrict__ mean,
                                                         const float* __restrict__ inv,
                                                         float* __restrict__ out,
                                                         const float* __restrict__ in_mean,
-                                                        const float* __restrict__ in_inv) {
+                                                        const float* __restrict__ in_inv,
+                                                        const int* __restrict__ vlen = nullptr,
+                                                        int vsh = 0) {
   __shared__ float red[TS][64][VN];
   __shared__ float mu_s[64][VN];
   const int cx = threadIdx.x & 63, ts = threadIdx.x >> 6;
@@ -1477,6 +1488,15 @@ __global__ __launch_bounds__(64 * TS, PRO ? 4 : 1) void stats_pool_k(const T* __
     w = r / chunks;
     ch = r - w * chunks;
   }
+  // rows pooled and time slices (RAG: per utterance; the block's 64 columns
+  // may span utterances, so per thread)
+  int Hp = H, tsn = TS;
+  if constexpr (RAG) {
+    Hp = valid_rows(vlen, vsh, n, H);
+    tsn = (sizeof(T) == 2 && VN == 8 && Hp <= 32) ? 1 : (Hp >= 64 ? 8 : (Hp >= 16 ? 4 : 1));
+    if (tsn > TS) tsn = TS;
+  }
+  const bool mine = valid && ts < tsn;
   const size_t rowstride = (size_t)W * C;
   const T* base = x + ((size_t)n * H * W + w) * C + (size_t)ch * VN;
   constexpr bool pro = PRO;
@@ -1499,11 +1519,12 @@ __global__ __launch_bounds__(64 * TS, PRO ? 4 : 1) void stats_pool_k(const T* __
   float s[VN];
 #pragma unroll
   for (int e = 0; e < VN; ++e) s[e] = 0.f;
-  if (valid) {
+  const int tstep = RAG ? tsn : TS;
+  if (mine) {
 #pragma unroll
     for (int i = 0; i < RM; ++i) {
-      const int h = ts + i * TS;
-      if (h < H) {
+      const int h = ts + i * tstep;
+      if (h < Hp) {
         const T* q = base + (size_t)h * rowstride;
         if constexpr (PK) {
           const bf16x8 r = ld16(q);
@@ -1523,7 +1544,7 @@ __global__ __launch_bounds__(64 * TS, PRO ? 4 : 1) void stats_pool_k(const T* __
     }
     // (unrolled: the loads of 4 rows issue together, the sums keep their order)
 #pragma unroll 4
-    for (int h = ts + RM * TS; h < H; h += TS) {
+    for (int h = ts + RM * tstep; h < Hp; h += tstep) {
       const T* q = base + (size_t)h * rowstride;
 #pragma unroll
       for (int e = 0; e < VN; ++e) s[e] += elt((float)q[e], e);
@@ -1535,36 +1556,36 @@ __global__ __launch_bounds__(64 * TS, PRO ? 4 : 1) void stats_pool_k(const T* __
   if (ts == 0) {
 #pragma unroll
     for (int e = 0; e < VN; ++e) {
-      float t = 0.f;
-      for (int k = 0; k < TS; ++k) t += red[k][cx][e];
-      mu_s[cx][e] = t / (float)H;
+      float t = RAG ? red[0][cx][e] : 0.f;
+      for (int k = RAG ? 1 : 0; k < (RAG ? tsn : TS); ++k) t += red[k][cx][e];
+      mu_s[cx][e] = t / (float)Hp;
     }
   }
   __syncthreads();
   float mu[VN];
 #pragma unroll
   for (int e = 0; e < VN; ++e) { mu[e] = mu_s[cx][e]; s[e] = 0.f; }
-  if (valid) {
+  if (mine) {
 #pragma unroll
     for (int i = 0; i < RM; ++i) {
-      if (ts + i * TS < H) {
+      if (ts + i * tstep < Hp) {
 #pragma unroll
         for (int e = 0; e < VN; ++e) {
           float x;
           if constexpr (PK) x = (float)vb[i][e];
           else x = v[i][e];
           const float d = x - mu[e];
-          s[e] += d * d;
+          s[e] = __builtin_fmaf(d, d, s[e]);   // explicit: one rounding in every pool variant
         }
       }
     }
 #pragma unroll 4
-    for (int h = ts + RM * TS; h < H; h += TS) {
+    for (int h = ts + RM * tstep; h < Hp; h += tstep) {
       const T* q = base + (size_t)h * rowstride;
 #pragma unroll
       for (int e = 0; e < VN; ++e) {
         float d = elt((float)q[e], e) - mu[e];
-        s[e] += d * d;
+        s[e] = __builtin_fmaf(d, d, s[e]);
       }
     }
   }
@@ -1576,9 +1597,9 @@ __global__ __launch_bounds__(64 * TS, PRO ? 4 : 1) void stats_pool_k(const T* __
     float* o = out + (size_t)n * W * 2 * C + (size_t)w * 2 * C + (size_t)ch * VN;
 #pragma unroll
     for (int e = 0; e < VN; ++e) {
-      float t = 0.f;
-      for (int k = 0; k < TS; ++k) t += red[k][cx][e];
-      float sd = sqrtf(t / (float)H + 1e-5f);
+      float t = RAG ? red[0][cx][e] : 0.f;
+      for (int k = RAG ? 1 : 0; k < (RAG ? tsn : TS); ++k) t += red[k][cx][e];
+      float sd = sqrtf(t / (float)Hp + 1e-5f);
       float m = mu[e];
       const int fm = w * 2 * C + ch * VN + e, fs = fm + C;
       if (mean) {
@@ -1663,7 +1684,7 @@ __global__ __launch_bounds__(256) void stats_pool_col(const bf16_t* __restrict__
 #pragma unroll
       for (int e = 0; e < VN; ++e) {
         const float d = (float)b[e] - mu[e];
-        q[e] += d * d;
+        q[e] = __builtin_fmaf(d, d, q[e]);   // as stats_pool_k (ragged batches pool there)
       }
     }
   float* o = out + (size_t)n * W * 2 * C + (size_t)w * 2 * C + (size_t)ch * VN;
@@ -1687,8 +1708,14 @@ __global__ __launch_bounds__(256) void stats_pool_col(const bf16_t* __restrict__
 template <typename T, int VN>
 static hipError_t stats_pool_ts(const T* x, int N, int H, int W, int C, const float* mean,
                                 const float* inv, float* out, const float* in_mean,
-                                const float* in_inv, hipStream_t s) {
+                                const float* in_inv, hipStream_t s, const int* vlen, int vsh) {
   const int64_t cols = (int64_t)N * W * (C / VN);
+  if (vlen) {   // ragged batch: per-utterance rows and slice counts (stats_pool_k RAG)
+    if (in_mean) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((stats_pool_k<T, VN, 8, false, true>), dim3((unsigned)((cols + 63) / 64)),
+                       dim3(64 * 8), 0, s, x, N, H, W, C, mean, inv, out, in_mean, in_inv, vlen, vsh);
+    return hipGetLastError();
+  }
   if constexpr (sizeof(T) == 2 && VN == 8) {
     if (H <= 32) {
       const unsigned b = (unsigned)((cols * 2 + 255) / 256);
@@ -1748,17 +1775,17 @@ static hipError_t stats_pool_ts(const T* x, int N, int H, int W, int C, const fl
 
 hipError_t launch_stats_pool(DType t, const void* x, int N, int H, int W, int C,
                              const float* mean, const float* inv, float* out, hipStream_t s,
-                             const float* in_mean, const float* in_inv) {
+                             const float* in_mean, const float* in_inv, const int* vlen, int vsh) {
   if (t == BF16) {
     if (C % 8 == 0)
-      return stats_pool_ts<bf16_t, 8>((const bf16_t*)x, N, H, W, C, mean, inv, out, in_mean, in_inv, s);
+      return stats_pool_ts<bf16_t, 8>((const bf16_t*)x, N, H, W, C, mean, inv, out, in_mean, in_inv, s, vlen, vsh);
     if (C % 2 == 0)
-      return stats_pool_ts<bf16_t, 2>((const bf16_t*)x, N, H, W, C, mean, inv, out, in_mean, in_inv, s);
-    return stats_pool_ts<bf16_t, 1>((const bf16_t*)x, N, H, W, C, mean, inv, out, in_mean, in_inv, s);
+      return stats_pool_ts<bf16_t, 2>((const bf16_t*)x, N, H, W, C, mean, inv, out, in_mean, in_inv, s, vlen, vsh);
+    return stats_pool_ts<bf16_t, 1>((const bf16_t*)x, N, H, W, C, mean, inv, out, in_mean, in_inv, s, vlen, vsh);
   }
   if (C % 4 == 0)
-    return stats_pool_ts<float, 4>((const float*)x, N, H, W, C, mean, inv, out, in_mean, in_inv, s);
-  return stats_pool_ts<float, 1>((const float*)x, N, H, W, C, mean, inv, out, in_mean, in_inv, s);
+    return stats_pool_ts<float, 4>((const float*)x, N, H, W, C, mean, inv, out, in_mean, in_inv, s, vlen, vsh);
+  return stats_pool_ts<float, 1>((const float*)x, N, H, W, C, mean, inv, out, in_mean, in_inv, s, vlen, vsh);
 }
 
 // ----------------------------------------------------------------------------
@@ -1790,7 +1817,8 @@ __global__ __launch_bounds__(256) void avgpool3s2_k(const T* __restrict__ x, int
 __device__ uint4 g_pool_zero[1] = {};
 __global__ __launch_bounds__(256) void avgpool3s2_v8(const bf16_t* __restrict__ x, int ldx, int N,
                                                      int H, int W, int C8, bf16_t* __restrict__ y,
-                                                     int ldy, int Ho, int Wo) {
+                                                     int ldy, int Ho, int Wo,
+                                                     const int* __restrict__ vlen, int vsh) {
   // 32-bit index math (the launcher guarantees N*Ho*Wo*C8 < 2^31): the 64-bit
   // divisions cost more than the loads
   const unsigned idx = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1801,13 +1829,14 @@ __global__ __launch_bounds__(256) void avgpool3s2_v8(const bf16_t* __restrict__ 
   const int wo = (int)(pix - nh * (unsigned)Wo);
   const int n = (int)(nh / (unsigned)Ho);
   const int ho = (int)(nh - (unsigned)n * (unsigned)Ho);
+  const int Hn = valid_rows(vlen, vsh, n, H);   // ragged batch: padding past the utterance
   // all nine taps requested at once (padding taps read a zero line and add an
   // exact +0: the same sums in the same order as skipping them)
   bf16x8 v[9];
 #pragma unroll
   for (int t = 0; t < 9; ++t) {
     const int hi = 2 * ho - 1 + t / 3, wi = 2 * wo - 1 + t % 3;
-    const bool ok = hi >= 0 && hi < H && wi >= 0 && wi < W;
+    const bool ok = hi >= 0 && hi < Hn && wi >= 0 && wi < W;
     v[t] = ld16(ok ? x + (((size_t)n * H + hi) * W + wi) * ldx + c
                    : reinterpret_cast<const bf16_t*>(g_pool_zero));
   }
@@ -1815,7 +1844,7 @@ __global__ __launch_bounds__(256) void avgpool3s2_v8(const bf16_t* __restrict__ 
 #pragma unroll
   for (int t = 0; t < 9; ++t) {
     const int hi = 2 * ho - 1 + t / 3, wi = 2 * wo - 1 + t % 3;
-    if (hi >= 0 && hi < H && wi >= 0 && wi < W) {
+    if (hi >= 0 && hi < Hn && wi >= 0 && wi < W) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) s[e] += (float)v[t][e];
     }
@@ -1827,14 +1856,16 @@ __global__ __launch_bounds__(256) void avgpool3s2_v8(const bf16_t* __restrict__ 
 }
 
 hipError_t launch_avgpool3s2(DType t, const void* x, int ldx, int N, int H, int W, int C,
-                             void* y, int ldy, int Ho, int Wo, hipStream_t s) {
+                             void* y, int ldy, int Ho, int Wo, hipStream_t s, const int* vlen,
+                             int vsh) {
   if (t == BF16 && C % 8 == 0 && ldx % 8 == 0 && ldy % 8 == 0 &&
       (int64_t)N * Ho * Wo * (C / 8) < (int64_t)1 << 31) {
     const int64_t n = (int64_t)N * Ho * Wo * (C / 8);
     hipLaunchKernelGGL(avgpool3s2_v8, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
-                       (const bf16_t*)x, ldx, N, H, W, C / 8, (bf16_t*)y, ldy, Ho, Wo);
+                       (const bf16_t*)x, ldx, N, H, W, C / 8, (bf16_t*)y, ldy, Ho, Wo, vlen, vsh);
     return hipGetLastError();
   }
+  if (vlen) return hipErrorInvalidValue;   // ragged batches: the 8-channel kernel only
   const int64_t n = (int64_t)N * Ho * Wo * C;
   const unsigned g = (unsigned)((n + 255) / 256);
   if (t == BF16)

@@ -106,6 +106,41 @@ class Extractor:
                                          C.c_void_p(out.data_ptr()), C.c_void_p(sh)))
         return out
 
+    def run_lens(self, x, lens):
+        """Ragged batch (host numpy): x [N,T,F] with utterance i's lens[i]
+        frames first and padding after (its values are ignored) -> [N,D], each
+        row equal to run() on that utterance alone at T = lens[i]
+        (vox_embed_lens; res2net bf16 plans)."""
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        if x.ndim != 3:
+            raise ValueError("expected [N, T, F] features")
+        n, t, f = x.shape
+        lens = np.ascontiguousarray(lens, dtype=np.int32)
+        if lens.shape != (n,):
+            raise ValueError("one length per utterance")
+        out = np.empty((n, self.dim), np.float32)
+        check(lib().vox_embed_lens(self._h, fptr(x), n, t, f, lens.ctypes.data, fptr(out)))
+        return out
+
+    def run_device_lens(self, x, lens, out=None, stream=None):
+        """run_device for a ragged batch: lens is an int32 device tensor [N]
+        (each in [1, T]; not checked on the device)."""
+        import torch
+        if x.dtype != torch.float32 or not x.is_contiguous() or x.dim() != 3:
+            raise ValueError("expected a contiguous float32 [N,T,F] device tensor")
+        n, t, f = x.shape
+        if lens.dtype != torch.int32 or lens.shape != (n,) or lens.device != x.device:
+            raise ValueError("expected an int32 [N] lengths tensor on the input's device")
+        if out is None:
+            out = torch.empty((n, self.dim), dtype=torch.float32, device=x.device)
+        if stream is None:
+            stream = torch.cuda.current_stream(x.device)
+        with self._ordered(stream, x.device) as sh:
+            check(lib().vox_embed_device_lens(self._h, C.c_void_p(x.data_ptr()), n, t, f,
+                                              C.c_void_p(lens.data_ptr()),
+                                              C.c_void_p(out.data_ptr()), C.c_void_p(sh)))
+        return out
+
     def _ordered(self, stream, device):
         """Context giving the raw handle to launch on for a torch stream (or raw
         handle).  The legacy default stream has handle 0, which the C-ABI reads
