@@ -242,6 +242,12 @@ int vox_mat_shapes(const char* const* paths, const int64_t* offsets, int n, int*
 int vox_read_chunks(const char* const* paths, const int64_t* offsets, const int* r0, const int* T,
                     const int* c0, const int* start, int n, int f, int len, int cmn_window,
                     float* out, int threads);
+/* The same for a ragged batch (vox_embed_lens): item i has lens[i] frames
+ * (1 <= lens[i] <= stride) and goes to out + i*stride*f; its rows from lens[i]
+ * to stride are left untouched (padding). */
+int vox_read_chunks_ragged(const char* const* paths, const int64_t* offsets, const int* r0,
+                           const int* T, const int* c0, const int* start, const int* lens, int n,
+                           int f, int stride, int cmn_window, float* out, int threads);
 /* Serialise "key \0BFV \4<u32 dim><dim f32>" into buf; returns bytes written
  * (or needed, if cap is too small) and the offset of "\0B" via *data_offset. */
 int64_t vox_format_vec_flt(const char* key, const float* v, int dim, uint8_t* buf,

@@ -857,13 +857,15 @@ def test_resident_plans_alternating_shapes(weights, monkeypatch):
         assert ex.plan_stats()["built"] == len(shapes) - 0 and ex.plan_stats()["resident"] == 1
 
 
-@pytest.mark.parametrize("lanes", [1, 3])
-def test_stream_lanes_equal_in_memory_path(weights, tmp_path, lanes):
+@pytest.mark.parametrize("lanes,ragged", [(1, True), (3, True), (1, False), (3, False)])
+def test_stream_lanes_equal_in_memory_path(weights, tmp_path, lanes, ragged):
     """The streaming pipeline (stream.extract_entries: header planning, native
     batched reader, `lanes` handles on their own streams) gives the same bits
     as decoding the whole shard and running the chunk loop through one
     handle's host API (the round-4 extract.py path), bf16 Res2Net, lengths
-    across the 1000-frame chunk boundary, batches of 3."""
+    across the 1000-frame chunk boundary, batches of 3 -- ragged batches
+    (chunks of different lengths padded together, vox_embed_device_lens) and
+    equal-length batches alike."""
     from voxsrc2020_speaker_verification_amd import extract, kaldi, synth
     from voxsrc2020_speaker_verification_amd.stream import extract_entries
     spec, t, blob = weights("res2net50_w24_s4_c32", 80)
@@ -876,7 +878,8 @@ def test_stream_lanes_equal_in_memory_path(weights, tmp_path, lanes):
     entries = kaldi.read_scp(str(tmp_path / "f.scp"))
     exs = [_extractor(blob, "bf16") for _ in range(lanes)]
     try:
-        keys, got = extract_entries(entries, exs, batch=3)
+        assert exs[0].supports_lengths()
+        keys, got = extract_entries(entries, exs, batch=3, ragged=ragged)
         stats = [e.plan_stats() for e in exs]
     finally:
         for e in exs:

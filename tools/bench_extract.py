@@ -62,30 +62,40 @@ def child(args):
              .Extractor(blob, device=0, precision="bf16") for _ in range(args.lanes)]
     entries = kaldi.read_scp(args.scp)
     torch.cuda.synchronize()
+    ragged = {"ragged": True, "exact": False, "auto": None}[args.mode]
+    if ragged is None:
+        ragged = lanes[0].supports_lengths()
+    st0 = [ex.plan_stats() for ex in lanes]
     t0 = time.perf_counter()
     table = stream.ChunkTable(entries, args.threads)
-    plans, batches = stream.plan_batches(table.T, args.batch, table.keys)
+    plans, batches = stream.plan_batches(table.T, args.batch, table.keys, ragged=ragged)
     t_plan = time.perf_counter() - t0
     keys, emb = stream.extract_stream(
-        table, lambda b: stream.LanePool(lanes, table, b), args.batch)
+        table, lambda b: stream.LanePool(lanes, table, b), args.batch, ragged=ragged)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     extract.write_vectors(args.wspec, keys, emb)
     t_write = time.perf_counter() - t1
     el = t1 - t0
     frames = int(table.T.sum())
-    st = [ex.plan_stats() for ex in lanes]
+    st = [{k: v - s0[k] for k, v in s1.items()} for s0, s1 in zip(st0, (ex.plan_stats() for ex in lanes))]
+    pad = sum(b[0] * len(b[1]) for b in batches)
     for ex in lanes:
         ex.close()
     print(json.dumps({
         "utts": len(keys), "frames": frames, "chunks": sum(len(p) for p in plans),
-        "batches": len(batches), "distinct_lengths": len({L for L, _ in batches}),
+        "batches": len(batches), "distinct_lengths": len({b[0] for b in batches}),
+        "mode": "ragged" if ragged else "exact", "padded_frames_frac": round(frames_chunks(plans) / pad, 4),
         "seconds": round(el, 4), "plan_s": round(t_plan, 4), "write_s": round(t_write, 4),
         "utt_per_s": round(len(keys) / el, 1), "frames_per_s": round(frames / el, 1),
         "plans_built": sum(s["built"] for s in st), "plan_hits": sum(s["hits"] for s in st),
         "plans_dropped": sum(s["dropped"] for s in st), "lanes": args.lanes,
         "batch": args.batch, "reader_threads": table.threads,
         "peak_rss_mb": round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024, 1)}))
+
+
+def frames_chunks(plans):
+    return sum(L for p in plans for _, L in p)
 
 
 def fixed_shape_fps(model, B=256, T=200, steps=10):
@@ -120,6 +130,8 @@ def main():
     ap.add_argument("--child", action="store_true")
     ap.add_argument("--scp", default=None)
     ap.add_argument("--wspec", default=None)
+    ap.add_argument("--mode", default="auto", choices=["auto", "ragged", "exact"],
+                    help="ragged batches (vox_embed_lens) or equal-length batches")
     args = ap.parse_args()
     if args.child:
         args.lanes = int(args.lanes)
@@ -140,7 +152,7 @@ def main():
                 continue   # the doubled set: RSS check at the last lane count only
             cmd = [sys.executable, os.path.abspath(__file__), "--child", "--scp", base + ".scp",
                    "--wspec", os.path.join(args.dir, f"xv{n}_{lanes}"), "--lanes", str(lanes),
-                   "--batch", str(args.batch), "--model", args.model]
+                   "--batch", str(args.batch), "--model", args.model, "--mode", args.mode]
             if args.threads:
                 cmd += ["--threads", str(args.threads)]
             r = subprocess.run(cmd, capture_output=True, text=True, cwd=ROOT)

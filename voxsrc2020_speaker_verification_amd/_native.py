@@ -84,6 +84,9 @@ _SIGS = [
     ("vox_read_chunks", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                   C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
                                   C.c_int]),
+    ("vox_read_chunks_ragged", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                         C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int,
+                                         C.c_int, C.c_int, C.c_void_p, C.c_int]),
     ("vox_parse_mat_kaldi", C.c_int, [C.c_char_p, C.c_size_t, _F, C.c_int, C.c_int,
                                       C.POINTER(C.c_size_t)]),
     ("vox_parse_mat_shape", C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(C.c_int),

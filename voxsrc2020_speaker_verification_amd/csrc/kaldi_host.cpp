@@ -414,10 +414,13 @@ extern "C" int vox_mat_shapes(const char* const* paths, const int64_t* offsets, 
   return prc;
 }
 
-extern "C" int vox_read_chunks(const char* const* paths, const int64_t* offsets, const int* r0,
-                               const int* T, const int* c0, const int* start, int n, int f,
-                               int len, int cmn_window, float* out, int threads) {
-  if (n < 0 || f <= 0 || len <= 0 || (n > 0 && (!paths || !offsets || !r0 || !T || !c0 || !start || !out)))
+// chunk i (lens ? lens[i] : len rows) at out + i * stride * f; rows past a
+// chunk's own length up to stride are left as they are (ragged batches)
+static int read_chunks(const char* const* paths, const int64_t* offsets, const int* r0,
+                       const int* T, const int* c0, const int* start, const int* lens, int n, int f,
+                       int len, int stride, int cmn_window, float* out, int threads) {
+  if (n < 0 || f <= 0 || stride <= 0 || (!lens && (len <= 0 || len > stride)) ||
+      (n > 0 && (!paths || !offsets || !r0 || !T || !c0 || !start || !out)))
     return kfail(VOX_EINVAL, "bad arguments");
   FirstError err;
   const int prc = parallel_for(n, threads, [&](int i) {
@@ -425,7 +428,9 @@ extern "C" int vox_read_chunks(const char* const* paths, const int64_t* offsets,
     auto bad = [&](int rc) {
       err.set(rc, (std::string(paths[i] ? paths[i] : "?") + ": " + vox_last_error()).c_str());
     };
-    if (!paths[i] || T[i] <= 0 || r0[i] < 0 || c0[i] < 0 || start[i] < 0 || start[i] + len > T[i])
+    const int clen = lens ? lens[i] : len;
+    if (clen <= 0 || clen > stride) return bad(kfail(VOX_EINVAL, "chunk length outside [1, stride]"));
+    if (!paths[i] || T[i] <= 0 || r0[i] < 0 || c0[i] < 0 || start[i] < 0 || start[i] + clen > T[i])
       return bad(kfail(VOX_EINVAL, "chunk outside its utterance"));
     thread_local std::vector<uint8_t> buf;
     thread_local std::vector<float> mat, utt;
@@ -445,12 +450,28 @@ extern "C" int vox_read_chunks(const char* const* paths, const int64_t* offsets,
         std::memcpy(&utt[(size_t)t * f], &mat[(size_t)(r0[i] + t) * cols + c0[i]], (size_t)f * 4);
       u = utt.data();
     }
-    float* o = out + (size_t)i * len * f;
+    float* o = out + (size_t)i * stride * f;
     if (cmn_window > 0)
-      sliding_cmn_rows(u, T[i], f, cmn_window, 1, start[i], start[i] + len, o);
+      sliding_cmn_rows(u, T[i], f, cmn_window, 1, start[i], start[i] + clen, o);
     else
-      std::memcpy(o, u + (size_t)start[i] * f, (size_t)len * f * 4);
+      std::memcpy(o, u + (size_t)start[i] * f, (size_t)clen * f * 4);
   });
   if (err.code.load()) return kfail(err.code.load(), err.msg.c_str());
   return prc;
+}
+
+extern "C" int vox_read_chunks(const char* const* paths, const int64_t* offsets, const int* r0,
+                               const int* T, const int* c0, const int* start, int n, int f,
+                               int len, int cmn_window, float* out, int threads) {
+  return read_chunks(paths, offsets, r0, T, c0, start, nullptr, n, f, len, len, cmn_window, out,
+                     threads);
+}
+
+extern "C" int vox_read_chunks_ragged(const char* const* paths, const int64_t* offsets,
+                                      const int* r0, const int* T, const int* c0, const int* start,
+                                      const int* lens, int n, int f, int stride, int cmn_window,
+                                      float* out, int threads) {
+  if (n > 0 && !lens) return kfail(VOX_EINVAL, "null lengths");
+  return read_chunks(paths, offsets, r0, T, c0, start, lens, n, f, 0, stride, cmn_window, out,
+                     threads);
 }

@@ -122,6 +122,18 @@ class Extractor:
         check(lib().vox_embed_lens(self._h, fptr(x), n, t, f, lens.ctypes.data, fptr(out)))
         return out
 
+    def supports_lengths(self):
+        """Whether this handle's plans take ragged batches (run_lens): probed
+        once with a two-utterance batch (res2net bf16 plans do)."""
+        if "_rag_ok" not in self.__dict__:
+            try:
+                x = np.zeros((2, 64, self.feat_dim), np.float32)
+                self.run_lens(x, [64, 40])
+                self._rag_ok = True
+            except _native.VoxError:
+                self._rag_ok = False
+        return self._rag_ok
+
     def run_device_lens(self, x, lens, out=None, stream=None):
         """run_device for a ragged batch: lens is an int32 device tensor [N]
         (each in [1, T]; not checked on the device)."""

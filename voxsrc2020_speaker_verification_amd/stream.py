@@ -6,10 +6,14 @@ into a Queue(32), and the session runs each <= 1000-frame chunk on its own
 (:96-108).  Here the same results come out of three stages that overlap:
 
   1. planning (headers only): every utterance's frame count from its matrix
-     header (`vox_mat_shapes`), the chunk rule (:96-107) applied, and the chunks
-     bucketed by length over the whole shard -- equal-length chunks batch
-     together bit for bit (embeddings are batch-independent), and the shard is
-     one planning window, so real length distributions still give full batches;
+     header (`vox_mat_shapes`), the chunk rule (:96-107) applied over the whole
+     shard (one planning window).  Ragged mode (res2net bf16, the default where
+     the plan supports it): the chunks sorted by length and cut into full
+     batches padded to a coarse length grid (padded_length), each chunk's
+     frame count passed to the kernels (vox_embed_device_lens) -- real length
+     distributions give full batches and resident plans; exact mode: equal-
+     length chunks batched together.  Either way a chunk's embedding is the
+     bits of its own unpadded run (batch independence, tests/test_ragged.py);
   2. reading: each batch's chunks decoded, CMN'd and sliced straight into a
      pinned host buffer by the native reader (`vox_read_chunks`, host threads)
      while the lane's previous batch runs on the GPU;
@@ -32,7 +36,7 @@ import os
 import numpy as np
 
 from ._native import check, lib
-from .extractor import MIN_FRAMES, chunk_plan
+from .extractor import MAX_FRAMES, MIN_FRAMES, chunk_plan
 from .kaldi import CMN_WINDOW, parse_rxfile
 
 
@@ -112,13 +116,47 @@ class ChunkTable:
                                     CMN_WINDOW if cmn else 0, C.c_void_p(ptr),
                                     threads or self.threads))
 
+    def read_ragged(self, items, lens, stride, out, cmn=True, threads=None):
+        """Chunks [(u, ci, start)] of lens[i] frames each into rows
+        [i*stride, i*stride + lens[i]) of out (a ragged batch; the rows after
+        each chunk are left as they are: padding)."""
+        n = len(items)
+        u = np.fromiter((it[0] for it in items), np.int64, n)
+        st = np.fromiter((it[2] for it in items), np.int32, n)
+        ln = np.ascontiguousarray(lens, dtype=np.int32)
+        paths = (C.c_char_p * n)(*[self._paths[i] for i in u])
+        offs = np.ascontiguousarray(self.offsets[u])
+        r0 = np.ascontiguousarray(self.r0[u])
+        T = np.ascontiguousarray(self.T[u])
+        c0 = np.ascontiguousarray(self.c0[u])
+        ptr = out.data_ptr() if hasattr(out, "data_ptr") else out.ctypes.data
+        check(lib().vox_read_chunks_ragged(paths, offs.ctypes.data, r0.ctypes.data, T.ctypes.data,
+                                           c0.ctypes.data, st.ctypes.data, ln.ctypes.data, n,
+                                           self.feat_dim, int(stride), CMN_WINDOW if cmn else 0,
+                                           C.c_void_p(ptr), threads or self.threads))
 
-def plan_batches(lengths, batch, keys=None):
-    """The chunk rule over every utterance, equal-length chunks bucketed:
-    -> (per-utterance chunk plans, [(L, [(u, ci, start), ...]), ...]).  Buckets
-    keep scp order inside; batches are ordered by size (frames) descending, so
-    the first batch sizes the device workspace once.  An utterance shorter than
-    25 frames raises ZeroDivisionError, as tf_extract.py:111 does."""
+
+def padded_length(L, max_frames=MAX_FRAMES):
+    """Row count a ragged batch whose longest chunk has L frames is padded to:
+    a grid of ~1/16 steps (8 frames up to 128, 16 up to 256, 32 up to 512, 64
+    beyond; the chunk maximum itself at the top), so batches of neighbouring
+    lengths share a resident plan (and its graph) while padding stays a few
+    per cent of the frames."""
+    q = 8 if L <= 128 else 16 if L <= 256 else 32 if L <= 512 else 64
+    Lp = -(-L // q) * q
+    return min(Lp, max(L, max_frames))
+
+
+def plan_batches(lengths, batch, keys=None, ragged=False):
+    """The chunk rule over every utterance -> (per-utterance chunk plans,
+    batches).  Exact mode: equal-length chunks bucketed, batches
+    (L, [(u, ci, start), ...]) with scp order inside a bucket.  Ragged mode
+    (vox_embed_lens): every chunk sorted by length, consecutive runs of `batch`
+    chunks padded to padded_length(longest) -> (Lp, items, lens); a chunk's
+    embedding is the same either way (bitwise: tests/test_ragged.py).
+    Batches are ordered by size (frames) descending, so the first sizes the
+    device workspace once.  An utterance shorter than 25 frames raises
+    ZeroDivisionError, as tf_extract.py:111 does."""
     plans, buckets = [], {}
     for u, T in enumerate(lengths):
         plan = chunk_plan(int(T))
@@ -129,8 +167,16 @@ def plan_batches(lengths, batch, keys=None):
         plans.append(plan)
         for ci, (s, L) in enumerate(plan):
             buckets.setdefault(L, []).append((u, ci, s))
-    batches = [(L, items[b:b + batch]) for L, items in buckets.items()
-               for b in range(0, len(items), batch)]
+    if ragged:
+        chunks = [(L, it) for L in sorted(buckets, reverse=True) for it in buckets[L]]
+        batches = []
+        for b in range(0, len(chunks), batch):
+            part = chunks[b:b + batch]
+            batches.append((padded_length(part[0][0]), [it for _, it in part],
+                            [L for L, _ in part]))
+    else:
+        batches = [(L, items[b:b + batch]) for L, items in buckets.items()
+                   for b in range(0, len(items), batch)]
     batches.sort(key=lambda b: -b[0] * len(b[1]))
     return plans, batches
 
@@ -194,8 +240,13 @@ class LanePool:
         self.table, self.cmn = table, cmn
         self.dev = torch.device("cuda", self.exs[0].device)
         F, dim, K = table.feat_dim, self.exs[0].dim, len(self.exs)
-        max_el = max((len(it) * L * F for L, it in batches), default=1)
-        max_n = max((len(it) for _, it in batches), default=1)
+        max_el = max((len(b[1]) * b[0] * F for b in batches), default=1)
+        max_n = max((len(b[1]) for b in batches), default=1)
+        # ragged batches (L, items, lens): per-lane device lengths + pinned copies
+        self.ragged = bool(batches) and len(batches[0]) == 3
+        self.d_len = [torch.empty(max_n, dtype=torch.int32, device=self.dev) for _ in range(K)]
+        self.h_len = [[torch.empty(max_n, dtype=torch.int32).pin_memory() for _ in range(2)]
+                      for _ in range(K)]
         self.threads = max(1, table.threads // K)
         self.streams = [torch.cuda.Stream(self.dev) for _ in range(K)]
         self.d_in = [torch.empty(max_el, dtype=torch.float32, device=self.dev) for _ in range(K)]
@@ -215,18 +266,30 @@ class LanePool:
             for i, b in enumerate(range(k, len(batches), len(self.exs))):
                 if stop:
                     return
-                L, items = batches[b]
+                L, items = batches[b][0], batches[b][1]
                 n, j = len(items), i & 1
                 if free[j] is not None:
                     free[j].synchronize()
                 hin = self.h_in[k][j]
-                self.table.read(items, L, hin, self.cmn, self.threads)
+                if self.ragged:
+                    lens = batches[b][2]
+                    self.table.read_ragged(items, lens, L, hin, self.cmn, self.threads)
+                    hl = self.h_len[k][j]
+                    hl[:n].copy_(torch.tensor(lens, dtype=torch.int32))
+                else:
+                    self.table.read(items, L, hin, self.cmn, self.threads)
                 x, o = self.d_in[k][:n * L * F], self.d_out[k][:n * dim]
+                dl = self.d_len[k][:n]
                 with torch.cuda.stream(s):
                     x.copy_(hin[:n * L * F], non_blocking=True)
+                    if self.ragged:
+                        dl.copy_(hl[:n], non_blocking=True)
                     free[j] = torch.cuda.Event()
                     free[j].record(s)
-                ex.run_device(x.view(n, L, F), o.view(n, dim), s)
+                if self.ragged:
+                    ex.run_device_lens(x.view(n, L, F), dl, o.view(n, dim), s)
+                else:
+                    ex.run_device(x.view(n, L, F), o.view(n, dim), s)
                 h = self.h_out[k][j]
                 with torch.cuda.stream(s):
                     h[:n * dim].copy_(o, non_blocking=True)
@@ -281,11 +344,12 @@ class LanePool:
             raise err
 
 
-def extract_stream(table, make_runner, batch=64):
+def extract_stream(table, make_runner, batch=64, ragged=False):
     """(keys, [N, dim] float32) of every utterance of `table`, in its order.
     make_runner(batches) -> an object whose run(batches) yields (batch index,
-    [n, dim] embeddings) in any order."""
-    plans, batches = plan_batches(table.T, batch, table.keys)
+    [n, dim] embeddings) in any order.  ragged: plan_batches' ragged mode (the
+    runner must take (L, items, lens) batches: LanePool)."""
+    plans, batches = plan_batches(table.T, batch, table.keys, ragged=ragged)
     comb = None
     for bid, rows in make_runner(batches).run(batches):
         if comb is None:
@@ -298,13 +362,19 @@ def extract_stream(table, make_runner, batch=64):
     return list(table.keys), comb.out
 
 
-def extract_entries(entries, extractors, batch=64, cmn=True, threads=None):
+def extract_entries(entries, extractors, batch=64, cmn=True, threads=None, ragged=None):
     """The GPU pipeline over scp entries [(key, rxfile)] with `extractors`
-    (one lane each: same device and weights) -> (keys, [N, dim] float32)."""
+    (one lane each: same device and weights) -> (keys, [N, dim] float32).
+    ragged: batch chunks of different lengths together (vox_embed_lens);
+    None = wherever the model's plan supports it (Extractor.supports_lengths),
+    else equal-length batches.  The embeddings are the same bits either way."""
     table = ChunkTable(entries, threads)
     dim = extractors[0].dim
     if not len(table):
         return [], np.zeros((0, dim), np.float32)
     if table.feat_dim != extractors[0].feat_dim:
         raise ValueError(f"feature dim {table.feat_dim} != model {extractors[0].feat_dim}")
-    return extract_stream(table, lambda batches: LanePool(extractors, table, batches, cmn), batch)
+    if ragged is None:
+        ragged = extractors[0].supports_lengths()
+    return extract_stream(table, lambda batches: LanePool(extractors, table, batches, cmn), batch,
+                          ragged=ragged)
