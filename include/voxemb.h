@@ -111,7 +111,8 @@ int vox_plan_describe(vox_model* m, const float* d_x, int n, int t, int f, char*
                       size_t cap);
 
 /* Plan residency counters of the handle: plans built (planned + captured),
- * calls served by a resident plan without re-planning, plans destroyed
+ * calls served by a resident plan (the current one or a cached one) without
+ * re-planning, plans destroyed
  * (evicted, or dropped when the workspace grew), and plans resident now
  * (current + cached; VOXEMB_PLAN_CACHE caps the cached ones, default 16).
  * Any pointer may be NULL. */

@@ -1891,8 +1891,10 @@ static int check_shape(vox_model* m, int n, int t, int f) {
 
 static int ensure_plan(vox_model* m, const float* d_x, int n, int t, float* d_out, bool rag = false) {
   if (m->plan_n == n && m->plan_t == t && m->plan_x == d_x && m->plan_out == d_out &&
-      m->plan_rag == rag)
+      m->plan_rag == rag) {
+    ++m->plan_hits;   // the current plan again (consecutive batches of one shape)
     return VOX_OK;
+  }
   for (PlanEntry& e : m->cache) {
     if (e.n != n || e.t != t || e.x != d_x || e.out != d_out || e.rag != rag) continue;
     // swap the resident plan in; the current one takes its cache entry
