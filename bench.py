@@ -455,6 +455,8 @@ def main():
         "traffic": traffic(dom_name),
         "traffic_unit": f"HBM bytes per launch (rocprofv3 PMC, profiles/{pmc_file})",
         "algorithmic_bytes_per_launch": dom["bytes"] / dom["n"],
+        "algorithmic_bytes_def": "input pixels sampled + output (+ residual) once, bf16, plus the "
+                                 "weights once per XCD (8 L2s)",
         "avg_launch_us": round(dom["ms"] / dom["n"] * 1e3, 2),
         "flop_per_launch": dom["flops"] / dom["n"],
         "mfma_tflops": round(ach, 2), "mfma_frac": round(ach / peak, 4),
@@ -491,7 +493,7 @@ def main():
             out32 = torch.empty((B, ex32.dim), dtype=torch.float32, device=dev)
             ex32.run_device(x, out32, stream)
             torch.cuda.synchronize(dev)
-            n32, t32 = 3, time.perf_counter()
+            n32, t32 = 10, time.perf_counter()
             for _ in range(n32):
                 ex32.run_device(x, out32, stream)
             torch.cuda.synchronize(dev)

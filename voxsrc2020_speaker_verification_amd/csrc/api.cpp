@@ -905,6 +905,11 @@ static void emit_conv(Builder& B, const ConvW& cw, Act x, const void* x2, int ld
   const double cols_in = std::min<double>(x.W, (double)Wo * std::min(cw.kw, sw) + (cw.kw > sw ? cw.kw - sw : 0));
   op.bytes = es * ((double)x.N * rows_in * cols_in * cw.cin * cw.groups * (x2 ? 2 : 1) +
                    (double)M * cw.cout * cw.groups * (res ? 2 : 1));
+  // + the weights once per XCD: each of the 8 XCDs' L2s fetches a layer's
+  // weights for its own workgroups (the floor once tiles spread over the chip;
+  // at B = 256 <= 0.5 % of a Res2Net 1x1's bytes, at the TDNN's B = 64 the
+  // k = 3 layers' 1.5 MB x 8 is a third of them, DESIGN.md "TDNN traffic")
+  op.bytes += 8.0 * es * (double)cw.groups * cw.cout * cw.cin * cw.kh * cw.kw;
   B.ops->push_back(op);
 }
 
