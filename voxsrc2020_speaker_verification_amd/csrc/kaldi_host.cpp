@@ -415,46 +415,90 @@ extern "C" int vox_mat_shapes(const char* const* paths, const int64_t* offsets, 
 }
 
 // chunk i (lens ? lens[i] : len rows) at out + i * stride * f; rows past a
-// chunk's own length up to stride are left as they are (ragged batches)
+// chunk's own length up to stride are left as they are (ragged batches).
+// The chunks of one utterance in a call (a long utterance's 1000-frame
+// chunks sort next to each other) are read, decoded and CMN'd once, by one
+// worker: the recursion runs to the last chunk's end and every chunk is a
+// slice of it (the same bits as one pass per chunk, sliding_cmn_rows).
 static int read_chunks(const char* const* paths, const int64_t* offsets, const int* r0,
                        const int* T, const int* c0, const int* start, const int* lens, int n, int f,
                        int len, int stride, int cmn_window, float* out, int threads) {
   if (n < 0 || f <= 0 || stride <= 0 || (!lens && (len <= 0 || len > stride)) ||
       (n > 0 && (!paths || !offsets || !r0 || !T || !c0 || !start || !out)))
     return kfail(VOX_EINVAL, "bad arguments");
-  FirstError err;
-  const int prc = parallel_for(n, threads, [&](int i) {
-    if (err.code.load()) return;
-    auto bad = [&](int rc) {
-      err.set(rc, (std::string(paths[i] ? paths[i] : "?") + ": " + vox_last_error()).c_str());
+  std::vector<int> order, gbeg;
+  try {
+    order.resize(n);
+    for (int i = 0; i < n; ++i) order[i] = i;
+    auto same = [&](int a, int b) {
+      return offsets[a] == offsets[b] && r0[a] == r0[b] && T[a] == T[b] && c0[a] == c0[b] &&
+             (paths[a] == paths[b] || (paths[a] && paths[b] && !std::strcmp(paths[a], paths[b])));
     };
-    const int clen = lens ? lens[i] : len;
-    if (clen <= 0 || clen > stride) return bad(kfail(VOX_EINVAL, "chunk length outside [1, stride]"));
-    if (!paths[i] || T[i] <= 0 || r0[i] < 0 || c0[i] < 0 || start[i] < 0 || start[i] + clen > T[i])
-      return bad(kfail(VOX_EINVAL, "chunk outside its utterance"));
+    // group equal utterances (stable: a group keeps its chunks' order)
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+      if (offsets[a] != offsets[b]) return offsets[a] < offsets[b];
+      const int c = std::strcmp(paths[a] ? paths[a] : "", paths[b] ? paths[b] : "");
+      if (c) return c < 0;
+      if (r0[a] != r0[b]) return r0[a] < r0[b];
+      if (T[a] != T[b]) return T[a] < T[b];
+      return c0[a] < c0[b];
+    });
+    for (int k = 0; k < n; ++k)
+      if (k == 0 || !same(order[k - 1], order[k])) gbeg.push_back(k);
+    gbeg.push_back(n);
+  } catch (...) {
+    return kfail(VOX_ENOMEM, "host allocation failed");
+  }
+  FirstError err;
+  const int ngroups = (int)gbeg.size() - 1;
+  const int prc = parallel_for(ngroups, threads, [&](int gi) {
+    if (err.code.load()) return;
+    const int first = order[gbeg[gi]];
+    auto bad = [&](int rc) {
+      err.set(rc, (std::string(paths[first] ? paths[first] : "?") + ": " + vox_last_error()).c_str());
+    };
+    // the group's rows [lo, hi) of the (ranged) utterance
+    int lo = 1 << 30, hi = 0;
+    for (int k = gbeg[gi]; k < gbeg[gi + 1]; ++k) {
+      const int i = order[k];
+      const int clen = lens ? lens[i] : len;
+      if (clen <= 0 || clen > stride) return bad(kfail(VOX_EINVAL, "chunk length outside [1, stride]"));
+      if (!paths[i] || T[i] <= 0 || r0[i] < 0 || c0[i] < 0 || start[i] < 0 || start[i] + clen > T[i])
+        return bad(kfail(VOX_EINVAL, "chunk outside its utterance"));
+      lo = std::min(lo, start[i]);
+      hi = std::max(hi, start[i] + clen);
+    }
     thread_local std::vector<uint8_t> buf;
-    thread_local std::vector<float> mat, utt;
-    int rc = read_file_at(paths[i], offsets[i], buf);
+    thread_local std::vector<float> mat, utt, cm;
+    int rc = read_file_at(paths[first], offsets[first], buf);
     if (rc) return bad(rc);
     Reader r{buf.data(), buf.size()};
     int rows, cols, kind;
     if ((rc = parse_header(r, &rows, &cols, &kind))) return bad(rc);
-    if (r0[i] + T[i] > rows || c0[i] + f > cols) return bad(kfail(VOX_EINVAL, "range outside the matrix"));
+    if (r0[first] + T[first] > rows || c0[first] + f > cols)
+      return bad(kfail(VOX_EINVAL, "range outside the matrix"));
     mat.resize((size_t)rows * cols);
     // Kaldi's CompressedMatrix arithmetic: what apply-cmvn-sliding decodes (tf_extract.py:63)
     if ((rc = parse_payload(r, kind, rows, cols, mat.data(), 1))) return bad(rc);
     const float* u = mat.data();
-    if (r0[i] != 0 || T[i] != rows || c0[i] != 0 || f != cols) {   // the rxfile's [range]
-      utt.resize((size_t)T[i] * f);
-      for (int t = 0; t < T[i]; ++t)
-        std::memcpy(&utt[(size_t)t * f], &mat[(size_t)(r0[i] + t) * cols + c0[i]], (size_t)f * 4);
+    if (r0[first] != 0 || T[first] != rows || c0[first] != 0 || f != cols) {   // the rxfile's [range]
+      utt.resize((size_t)T[first] * f);
+      for (int t = 0; t < T[first]; ++t)
+        std::memcpy(&utt[(size_t)t * f], &mat[(size_t)(r0[first] + t) * cols + c0[first]], (size_t)f * 4);
       u = utt.data();
     }
-    float* o = out + (size_t)i * stride * f;
-    if (cmn_window > 0)
-      sliding_cmn_rows(u, T[i], f, cmn_window, 1, start[i], start[i] + clen, o);
-    else
-      std::memcpy(o, u + (size_t)start[i] * f, (size_t)clen * f * 4);
+    const float* rowsrc = u + (size_t)lo * f;   // row lo of the (CMN'd) utterance
+    if (cmn_window > 0) {
+      cm.resize((size_t)(hi - lo) * f);
+      sliding_cmn_rows(u, T[first], f, cmn_window, 1, lo, hi, cm.data());
+      rowsrc = cm.data();
+    }
+    for (int k = gbeg[gi]; k < gbeg[gi + 1]; ++k) {
+      const int i = order[k];
+      const int clen = lens ? lens[i] : len;
+      std::memcpy(out + (size_t)i * stride * f, rowsrc + (size_t)(start[i] - lo) * f,
+                  (size_t)clen * f * 4);
+    }
   });
   if (err.code.load()) return kfail(err.code.load(), err.msg.c_str());
   return prc;
