@@ -211,6 +211,9 @@ int vox_debug_taps(vox_model* m, const float* d_x, int n, int t, int f, float* d
                    vox_tap* taps, int max_taps, int* n_ops);
 int vox_debug_run_ops(vox_model* m, int op_begin, int op_end, void* stream);
 int vox_debug_read(void* dst, const void* d_src, size_t bytes);
+/* sizeof of an internal kernel parameter struct (0 = BneckParams, 1 = GconvParams),
+ * for tests that launch a kernel through a ctypes mirror of it; -1 otherwise. */
+int64_t vox_debug_struct_size(int which);
 
 /* ---- host-side Kaldi I/O (no Kaldi binaries needed) --------------------- */
 int vox_sliding_cmn(const float* in, int t, int f, int cmn_window, int center,

@@ -27,7 +27,8 @@ class BneckParams(C.Structure):
                 ("wa", C.c_void_p), ("ma", C.c_void_p), ("ia", C.c_void_p),
                 ("wb", C.c_void_p * 8), ("mb", C.c_void_p * 8), ("ib", C.c_void_p * 8),
                 ("wc", C.c_void_p), ("mc", C.c_void_p), ("ic", C.c_void_p),
-                ("wp", C.c_void_p), ("mp", C.c_void_p), ("ip", C.c_void_p), ("dbg", C.c_int)]
+                ("wp", C.c_void_p), ("mp", C.c_void_p), ("ip", C.c_void_p), ("dbg", C.c_int),
+                ("vlen", C.c_void_p), ("vsh", C.c_int)]
 
 
 def paired(wio):
@@ -110,6 +111,7 @@ def _block(N, H, W, nseg, seed, Ci=128):
     q.wc, q.mc, q.ic = wc_d.data_ptr(), keep[2].data_ptr(), keep[3].data_ptr()
     q.wp, q.mp, q.ip = wp_d.data_ptr(), mp_d.data_ptr(), ip_d.data_ptr()
     q.dbg = 0
+    q.vlen, q.vsh = None, 0          # every row valid (ragged batches: kernels.h)
     fn = getattr(_native.lib(), "_ZN3vox12launch_bneckERKNS_11BneckParamsEiiiiP12ihipStream_t")
     fn.restype = C.c_int
     fn.argtypes = [C.POINTER(BneckParams), C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]

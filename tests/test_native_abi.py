@@ -48,3 +48,21 @@ def test_bad_blob_rejected_before_device():
     blob = b"VOXEMB01" + (10 ** 9).to_bytes(8, "little")
     h = C.c_void_p()
     assert _native.lib().vox_load_blob(blob, len(blob), 0, 1, C.byref(h)) == _native.VOX_EIO
+
+
+def test_kernel_param_mirrors_match_the_library():
+    """The GPU unit tests launch bneck_fused / gconv3x3_rows through ctypes
+    mirrors of their parameter structs: a mirror shorter than the C++ struct
+    makes the kernel read past it (round 6: an illegal address when
+    BneckParams grew).  Their sizes must equal the library's."""
+    import ctypes as C
+    import importlib.util
+    import os
+    from voxsrc2020_speaker_verification_amd._native import lib
+    here = os.path.dirname(os.path.abspath(__file__))
+    for which, (mod, cls) in enumerate([("test_bneck_unit", "BneckParams"),
+                                         ("test_gconv_unit", "GconvParams")]):
+        spec = importlib.util.spec_from_file_location(mod, os.path.join(here, mod + ".py"))
+        m = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(m)
+        assert C.sizeof(getattr(m, cls)) == lib().vox_debug_struct_size(which), cls

@@ -74,6 +74,7 @@ _SIGS = [
                                  C.POINTER(Tap), C.c_int, C.POINTER(C.c_int)]),
     ("vox_debug_run_ops", C.c_int, [_P, C.c_int, C.c_int, _P]),
     ("vox_debug_read", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
+    ("vox_debug_struct_size", C.c_int64, [C.c_int]),
     ("vox_sliding_cmn", C.c_int, [_F, C.c_int, C.c_int, C.c_int, C.c_int, _F]),
     ("vox_mat_shape", C.c_int, [C.c_char_p, C.c_int64, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     ("vox_read_mat", C.c_int, [C.c_char_p, C.c_int64, _F, C.c_int, C.c_int]),

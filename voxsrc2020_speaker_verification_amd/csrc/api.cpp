@@ -2354,6 +2354,10 @@ extern "C" int vox_debug_run_ops(vox_model* m, int op_begin, int op_end, void* s
   return VOX_OK;
 }
 
+extern "C" int64_t vox_debug_struct_size(int which) {
+  return which == 0 ? (int64_t)sizeof(BneckParams) : which == 1 ? (int64_t)sizeof(GconvParams) : -1;
+}
+
 extern "C" int vox_debug_read(void* dst, const void* d_src, size_t bytes) {
   if (!dst || !d_src) return fail(VOX_EINVAL, "null argument");
   HIPCHK(hipMemcpy(dst, d_src, bytes, hipMemcpyDeviceToHost));
