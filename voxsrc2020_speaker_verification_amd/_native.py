@@ -136,6 +136,10 @@ def lib():
     except OSError as e:
         raise NativeUnavailable(f"cannot load {LIB_PATH}: {e}") from e
     for name, res, args in _SIGS:
+        # an older build loaded for an A/B (tools/ab_libs.sh, VOXEMB_LIB) may lack
+        # entry points added since; the product library must have them all
+        if "VOXEMB_LIB" in os.environ and not hasattr(h, name):
+            continue
         fn = getattr(h, name)
         fn.restype = res
         fn.argtypes = args
