@@ -42,6 +42,10 @@ def _hipcc():
     raise RuntimeError("hipcc not found")
 
 
+# what the last build() call did: sources compiled, relinked, seconds
+LAST_BUILD = {}
+
+
 def build(verbose=False, force=False, diag=False) -> str:
     outdir = os.path.join(HERE, "..", "build", "native_diag" if diag else "native")
     lib = DIAG_LIB if diag else LIB
@@ -63,6 +67,11 @@ def build(verbose=False, force=False, diag=False) -> str:
         lang = ["-x", "hip"] if src.endswith(".hip") else []
         jobs.append([hipcc, f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-c", *lang,
                      path, "-o", obj, *flags, *dflags])
+    import time
+    t0 = time.perf_counter()
+    LAST_BUILD.clear()
+    LAST_BUILD.update(compiled=[os.path.basename(j[j.index("-c") + (3 if j[j.index("-c") + 1] == "-x" else 1)])
+                                for j in jobs], forced=bool(force), diag=bool(diag))
     if jobs:
         from concurrent.futures import ThreadPoolExecutor
 
@@ -75,9 +84,11 @@ def build(verbose=False, force=False, diag=False) -> str:
             list(pool.map(_cc, jobs))
         relink = True
     if not relink and all(os.path.getmtime(lib) >= os.path.getmtime(o) for o in objs):
+        LAST_BUILD.update(relinked=False, seconds=round(time.perf_counter() - t0, 1), lib=lib)
         return lib
     cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib, *objs]
     subprocess.run(cmd, check=True)
+    LAST_BUILD.update(relinked=True, seconds=round(time.perf_counter() - t0, 1), lib=lib)
     return lib
 
 
