@@ -107,3 +107,28 @@ def test_ragged_unsupported_plans_refuse(weights):
             ex.run_lens(x, [64, 65])                # longer than the batch
         with pytest.raises(VoxError):
             ex.run_lens(x, [0, 64])
+
+
+@pytest.mark.parametrize("name,F", [("res2net50_w24_s4_c32", 40), ("res2net50_w24_s4_c64", 80),
+                                    ("res2net50_w8_s6_c16", 40)])
+def test_ragged_other_res2nets(weights, name, F):
+    """Other Res2Net geometries: where the plan takes ragged batches
+    (supports_lengths) every row equals its exact run; where it does not (a
+    kernel that does not mask padded rows), run_lens refuses -- never a wrong
+    answer."""
+    from voxsrc2020_speaker_verification_amd._native import VoxError
+    from voxsrc2020_speaker_verification_amd.extractor import Extractor
+    spec, t, blob = weights(name, F)
+    lens = [120, 119, 113, 97, 64, 25]
+    x = _batch(lens, 120, F, np.random.default_rng(9))
+    with Extractor(blob, precision="bf16") as ex:
+        if name == "res2net50_w24_s4_c32":
+            assert ex.supports_lengths()        # the 40-d headline geometry must
+        if not ex.supports_lengths():
+            with pytest.raises(VoxError):
+                ex.run_lens(x, lens)
+            return
+        got = ex.run_lens(x, lens)
+        exp = _exact(ex, x, lens)
+        bad = [lens[i] for i in range(len(lens)) if not np.array_equal(got[i], exp[i])]
+        assert not bad, bad

@@ -276,45 +276,45 @@ struct vox_model {
   // Read once at load from the environment through kPlanEnv (below); each
   // names the kernel it turns off and the path taken instead.
   int no_win = 0;          // VOXEMB_NO_WIN: conv_win off (generic implicit GEMM)
-  int no_rr = 0;           // VOXEMB_NO_RR: conv1x1_rr off
+  int no_rr = 0;           // fixed (env switch removed in round 6); when set: conv1x1_rr off
   int no_gemm = 0;         // VOXEMB_NO_GEMM: the LDS GEMMs off (conv1x1_rr)
   int no_gemm_pipe = 0;    // VOXEMB_NO_GEMM_PIPE: gemm1x1_lds instead of gemm1x1_pipe
   int no_gemm_wide = 0;    // VOXEMB_NO_GEMM_WIDE: gemm1x1_pipe instead of gemm1x1_ws
-  int no_wblk = 0;         // VOXEMB_NO_WBLK: gemm1x1_ws reads the paired-row weights
+  int no_wblk = 0;         // fixed (env switch removed in round 6); when set: gemm1x1_ws reads the paired-row weights
   int no_s2_fused = 0;     // VOXEMB_NO_S2_FUSED: 1x1a + split_s2_rows instead of s2_fused
   int no_chain_fused = 0;  // VOXEMB_NO_CHAIN_FUSED: 1x1a + chain_rows instead of chain_fused
   int no_conv3_rw = 0;     // VOXEMB_NO_CONV3_RW: conv3x3_pipe for the w = 96 stride-1 branches
   int no_conv3_ks = 0;     // VOXEMB_NO_CONV3_KS: conv3x3_rw (not K-split) for them
   int no_conv3_utt = 0;    // VOXEMB_NO_CONV3_UTT: conv3x3_pipe for the w = 192 stride-1 branches
   int no_conv3_s2r = 0;    // VOXEMB_NO_CONV3_S2R: conv3x3_pipe for the w = 96 stride-2 branches
-  int no_gconv = 0;        // VOXEMB_NO_GCONV: grouped 3x3 on the generic implicit GEMM
-  int gconv_rs = 0;        // VOXEMB_GCONV_RS: grouped 3x3 output rows per step (0 = default)
-  int gconv_wgs = 1024;    // VOXEMB_GCONV_WGS: grouped 3x3 workgroups the row segments aim for
+  int no_gconv = 0;        // fixed (env switch removed in round 6); when set: grouped 3x3 on the generic implicit GEMM
+  int gconv_rs = 0;        // fixed (env switch removed in round 6); when set: grouped 3x3 output rows per step (0 = default)
+  int gconv_wgs = 1024;    // fixed (env switch removed in round 6); when set: grouped 3x3 workgroups the row segments aim for
                            // (1,024: 2 segments per utterance at stage 3, 1,453 -> 1,424 us
                            // over its 11 launches against 2,048)
   int no_conv3 = 0;        // VOXEMB_NO_CONV3: every 3x3 branch kernel off
   int no_gemm_pro = 0;     // VOXEMB_NO_GEMM_PRO: prologue 1x1 convs off the LDS-DMA GEMMs
   int no_gemm_taps = 0;    // VOXEMB_NO_GEMM_TAPS: TDNN dilated convs off gemm1x1_ws
-  int no_smallk = 0;       // VOXEMB_NO_SMALLK: DPN 10-channel 1x1s on the generic conv
+  int no_smallk = 0;       // fixed (env switch removed in round 6); when set: DPN 10-channel 1x1s on the generic conv
   int smallk_v1 = 0;       // VOXEMB_SMALLK_V1: conv1x1_smallk (version 1) instead of version 2
   int no_nw = 0;           // VOXEMB_NO_NW: narrow 1x1s on conv1x1_rr instead of conv1x1_nw
   int no_dpn_block = 0;    // VOXEMB_NO_DPN_BLOCK: DPN stage-1 blocks as 1x1a / gconv / 1x1c launches
   int dpn_nseg = 0;        // VOXEMB_DPN_NSEG: force dpn_block_rows' segments per utterance (tests)
   int dpn_dbg = 0;         // VOXEMB_DPN_DBG: dpn_block_rows diagnostics (VOX_DIAG builds)
   int no_pool_pro = 0;     // VOXEMB_NO_POOL_PRO: DPN68's final BN+ReLU as its own pass before the pool
-  int pro_min_cout = 192;  // VOXEMB_PRO_MIN_COUT: narrowest prologue 1x1 on gemm1x1_ws
+  int pro_min_cout = 192;  // fixed (env switch removed in round 6); when set: narrowest prologue 1x1 on gemm1x1_ws
   int gemm_ksub1 = 0;      // VOXEMB_GEMM_KSUB1: gemm1x1_ws's 128-pixel tiles with one k-step
                            // per ring slot instead of two (bitwise A/B)
   int gemm_var = 0;        // VOXEMB_GEMM_VAR: -1 = gemm1x1_wide instead of gemm1x1_ws
                            // (bitwise A/B); other values are diagnostics (VOX_DIAG builds)
-  int gemm_min_k = 128;    // VOXEMB_GEMM_MIN_K: smallest K routed to the LDS GEMMs (the K = 128
+  int gemm_min_k = 128;    // fixed (env switch removed in round 6); when set: smallest K routed to the LDS GEMMs (the K = 128
                            // L2 projection: gemm1x1_ws 0.17 ms vs conv1x1_rr 0.26 ms)
   int no_chain = 0;        // VOXEMB_NO_CHAIN: unfused Res2Net branches
   int no_stem = 0;         // VOXEMB_NO_STEM: stem through the generic conv
   int no_bneck = 0;        // VOXEMB_NO_BNECK: unfused identity bottlenecks
   int no_chain_rows = 0;   // VOXEMB_NO_CHAIN_ROWS: row-tiled split_chain instead
   int no_split_s2 = 0;     // VOXEMB_NO_SPLIT_S2: stride-2 branches as separate convs
-  int bneck_nseg = 0;      // VOXEMB_BNECK_NSEG: force row segments per utterance (tests)
+  int bneck_nseg = 0;      // fixed (env switch removed in round 6); when set: force row segments per utterance (tests)
   int bneck_dbg = 0;       // VOXEMB_BNECK_DBG: diagnostics (VOX_DIAG builds; skips work)
   int num_cu = 256;        // compute units (persistent grids)
 };
@@ -326,40 +326,31 @@ struct PlanEnv {
 };
 static const PlanEnv kPlanEnv[] = {
     {"VOXEMB_NO_WIN", &vox_model::no_win},
-    {"VOXEMB_NO_RR", &vox_model::no_rr},
     {"VOXEMB_NO_GEMM", &vox_model::no_gemm},
     {"VOXEMB_NO_GEMM_PIPE", &vox_model::no_gemm_pipe},
     {"VOXEMB_NO_GEMM_WIDE", &vox_model::no_gemm_wide},
-    {"VOXEMB_NO_WBLK", &vox_model::no_wblk},
     {"VOXEMB_NO_S2_FUSED", &vox_model::no_s2_fused},
     {"VOXEMB_NO_CHAIN_FUSED", &vox_model::no_chain_fused},
     {"VOXEMB_NO_CONV3_RW", &vox_model::no_conv3_rw},
     {"VOXEMB_NO_CONV3_KS", &vox_model::no_conv3_ks},
     {"VOXEMB_NO_CONV3_UTT", &vox_model::no_conv3_utt},
     {"VOXEMB_NO_CONV3_S2R", &vox_model::no_conv3_s2r},
-    {"VOXEMB_NO_GCONV", &vox_model::no_gconv},
-    {"VOXEMB_GCONV_RS", &vox_model::gconv_rs},
-    {"VOXEMB_GCONV_WGS", &vox_model::gconv_wgs},
     {"VOXEMB_NO_CONV3", &vox_model::no_conv3},
     {"VOXEMB_NO_GEMM_PRO", &vox_model::no_gemm_pro},
     {"VOXEMB_NO_GEMM_TAPS", &vox_model::no_gemm_taps},
-    {"VOXEMB_NO_SMALLK", &vox_model::no_smallk},
     {"VOXEMB_SMALLK_V1", &vox_model::smallk_v1},
     {"VOXEMB_NO_NW", &vox_model::no_nw},
     {"VOXEMB_NO_DPN_BLOCK", &vox_model::no_dpn_block},
     {"VOXEMB_DPN_NSEG", &vox_model::dpn_nseg},
     {"VOXEMB_DPN_DBG", &vox_model::dpn_dbg},
     {"VOXEMB_NO_POOL_PRO", &vox_model::no_pool_pro},
-    {"VOXEMB_PRO_MIN_COUT", &vox_model::pro_min_cout},
     {"VOXEMB_GEMM_VAR", &vox_model::gemm_var},
     {"VOXEMB_GEMM_KSUB1", &vox_model::gemm_ksub1},
-    {"VOXEMB_GEMM_MIN_K", &vox_model::gemm_min_k},
     {"VOXEMB_NO_CHAIN", &vox_model::no_chain},
     {"VOXEMB_NO_STEM", &vox_model::no_stem},
     {"VOXEMB_NO_BNECK", &vox_model::no_bneck},
     {"VOXEMB_NO_CHAIN_ROWS", &vox_model::no_chain_rows},
     {"VOXEMB_NO_SPLIT_S2", &vox_model::no_split_s2},
-    {"VOXEMB_BNECK_NSEG", &vox_model::bneck_nseg},
     {"VOXEMB_BNECK_DBG", &vox_model::bneck_dbg},
 };
 
