@@ -9,6 +9,8 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -27,9 +29,10 @@ def _line(r):
     return json.loads(lines[0])
 
 
-def test_gpus_2_spawns_two_ranks():
-    line = _line(_run(["--gpus", "2", "--steps", "3", "--stub-extractor"]))
-    assert line["n_gpus"] == 2 and line["ranks_ran"] == 2
+@pytest.mark.parametrize("n", [2, 4])
+def test_gpus_n_spawns_n_ranks(n):
+    line = _line(_run(["--gpus", str(n), "--steps", "3", "--stub-extractor"]))
+    assert line["n_gpus"] == n and line["ranks_ran"] == n
 
 
 def test_gpus_1_runs_in_process():
