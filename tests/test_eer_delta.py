@@ -88,4 +88,6 @@ def test_eer_delta_bf16_vs_fp32_and_oracle():
     assert 0.0 < r32[0] < 0.25                        # the task discriminates
     assert res["subset"]["score_max_abs_diff_gpu_fp32_vs_cpu"] <= 1e-4
     assert scpu[0] == s32[0]                          # same trials -> same EER at fp32
-    assert abs(r16[0] - r32[0]) <= 0.005              # bf16 moves the EER by < 0.5 % absolute
+    # bf16 against the fp32 path: within north_star's +-0.02 % absolute (box run:
+    # -0.0016 %, profiles/r06_eer_delta.json; deterministic inputs and kernels)
+    assert abs(r16[0] - r32[0]) <= 0.0002
