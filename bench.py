@@ -317,6 +317,44 @@ def stub_rank(args, world, rank):
     dist.destroy_process_group()
 
 
+def eer_delta(device, S=64, U=16, T=200, F=80):
+    """The metric's "EER delta vs ref" on what the box has (no VoxCeleb, no
+    trained graph): synthetic speakers -- a fixed smooth spectral envelope per
+    speaker plus per-utterance noise -- through a well-conditioned random-init
+    res2net50_w24_s4_c32, the bf16 product path against the fp32 parity path
+    (which tests/test_eer_delta.py pins to the C++ oracle), every target pair
+    against every non-target pair (tests/test_eer_delta.py: the same task)."""
+    import io as _io
+    from voxsrc2020_speaker_verification_amd import archs, scoring, synth, weights
+    from voxsrc2020_speaker_verification_amd.extractor import Extractor
+    spec = archs.get_arch("res2net50_w24_s4_c32", F)
+    t = synth.make_weights(spec, seed=1, calib_n=8, calib_T=120, residual_gain=0.25)
+    buf = _io.BytesIO()
+    weights.save_blob(buf, spec, t)
+    rng = np.random.default_rng(2020)
+    k = np.exp(-0.5 * (np.arange(-6, 7) / 2.5) ** 2)
+    k /= k.sum()
+    env = np.stack([np.convolve(e, k, mode="same") for e in rng.standard_normal((S, F))]) * 3
+    x = (env[:, None, None, :] + rng.standard_normal((S, U, T, F)) * 1.5).astype(np.float32)
+    x = x.reshape(S * U, T, F)
+    lab = np.repeat(np.arange(S), U)
+    iu = np.triu_indices(S * U, 1)
+    y = (lab[iu[0]] == lab[iu[1]]).astype(int)
+    res = {}
+    for prec in ("bf16", "fp32"):
+        with Extractor(buf.getvalue(), device=device, precision=prec) as ex:
+            e = ex.run(x)
+        e = e / np.linalg.norm(e, axis=1, keepdims=True)
+        eer, _, mindcf, _ = scoring.compute_eer_and_min_dcf(y, (e @ e.T)[iu].astype(np.float64))
+        res[prec] = (float(eer), float(mindcf))
+    return {"task": f"synthetic speakers, {S}x{U} utterances {F}x{T}, well-conditioned "
+                    "random-init weights (not VoxCeleb: no data or trained graph here)",
+            "target_trials": int(y.sum()), "nontarget_trials": int(len(y) - y.sum()),
+            "eer_bf16": round(res["bf16"][0], 6), "eer_fp32_ref": round(res["fp32"][0], 6),
+            "delta_eer_abs": round(res["bf16"][0] - res["fp32"][0], 6),
+            "mindcf_bf16": round(res["bf16"][1], 5), "mindcf_fp32_ref": round(res["fp32"][1], 5)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1,
@@ -330,6 +368,7 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-eer", action="store_true", help="skip the synthetic-speaker EER delta")
     ap.add_argument("--dump-ops", action="store_true", help="print per-op timing to stderr")
     ap.add_argument("--cache-dir", default=os.environ.get("VOXEMB_CACHE", "/tmp/voxemb_cache"))
     ap.add_argument("--stub-extractor", action="store_true", help=argparse.SUPPRESS)
@@ -506,6 +545,13 @@ def main():
                         "precision); the bf16 line's ratio is ratio_bf16_to_cpu"}
             cpu["ratio_bf16_to_cpu"] = round(value / cpu["value"], 2)
 
+    eer = None
+    # beside the CPU baseline (both reference comparisons; the profiling runs pass
+    # --no-cpu-baseline and so keep their dispatch lists to the timed workload)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.no_eer \
+            and args.model == "res2net50_w24_s4_c32" and args.precision == "bf16":
+        eer = eer_delta(dev.index, F=F)
+
     if rank == 0:
         line = {
             "metric": "utterances/sec (80-d FBANK, T=200) embedding extraction",
@@ -519,6 +565,7 @@ def main():
                        "parallelism": f"dp{world}" + (" + RCCL all-gather" if dist_on else "")},
             "roofline": roof,
             "cpu_baseline": cpu,
+            "eer_delta_vs_fp32": eer,
             **extra,
         }
         print(json.dumps(line))
