@@ -271,24 +271,42 @@ def launch_ranks(n, argv):
     GPU, as torchrun would and as eval_inference_model.sh:29-36 starts
     `num_gpus` tf_extract.py processes) and return the worst exit code.  Runs
     in the parent before anything touches the GPU; the parent never execs."""
+    import signal
     import subprocess
+
+    def _term(signum, frame):   # a launcher stopped from outside stops its ranks too
+        raise SystemExit(128 + signum)
+    signal.signal(signal.SIGTERM, _term)
     port = str(_free_port())
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
                    LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
-    codes = []
+    # a rank that fails leaves the others blocked in a collective: stop them
+    bad = None
     try:
-        for p in procs:
-            codes.append(p.wait())
+        while True:
+            alive = [p.poll() is None for p in procs]      # poll every rank (no short cut)
+            if not any(alive):
+                break
+            failed = [p.returncode for p in procs if p.returncode not in (None, 0)]
+            if failed:
+                bad = failed[0]
+                break
+            time.sleep(0.2)
     finally:
         for p in procs:
             if p.poll() is None:
-                p.kill()
-                p.wait()
-    bad = [c for c in codes if c != 0]
-    return bad[0] if bad else 0
+                p.terminate()
+                try:
+                    p.wait(timeout=20)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+    if bad is None:
+        bad = next((p.returncode for p in procs if p.returncode != 0), 0)
+    return bad
 
 
 def stub_rank(args, world, rank):
@@ -297,6 +315,8 @@ def stub_rank(args, world, rank):
     runs N ranks and that the line's n_gpus is the ranks that ran."""
     import torch
     import torch.distributed as dist
+    if os.environ.get("VOXEMB_STUB_FAIL_RANK") == str(rank):   # tests: a rank that dies
+        raise SystemExit(3)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     x = bench_features(2, args.frames, args.feat_dim, rank)
     out = torch.from_numpy(np.concatenate([x.mean(1), x.std(1)], 1).astype(np.float32))

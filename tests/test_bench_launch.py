@@ -50,3 +50,14 @@ def test_world_size_mismatch_exits_nonzero():
 def test_launch_failure_propagates():
     r = _run(["--gpus", "2", "--steps", "1", "--stub-extractor", "--frames", "-5"])
     assert r.returncode != 0
+
+
+def test_one_failing_rank_stops_the_others():
+    """A rank that dies (here: rank 1 of 2 before the rendezvous completes) must
+    not leave rank 0 blocked in the collective: the launcher stops it and exits
+    non-zero, well inside the test's time limit."""
+    import time
+    t0 = time.perf_counter()
+    r = _run(["--gpus", "2", "--steps", "1", "--stub-extractor"], VOXEMB_STUB_FAIL_RANK="1")
+    assert r.returncode != 0
+    assert time.perf_counter() - t0 < 120
