@@ -85,7 +85,8 @@ int vox_embed_device(vox_model* m, const float* d_x, int n, int t, int f,
  * pool averages its lens[i] (downsampled) rows.  So chunks of different
  * lengths share one batch and one resident plan keyed on (n, t) -- what the
  * streaming extractor buckets real length distributions into.  res2net models
- * without attentive pooling in VOX_BF16; other plans return VOX_EINVAL.
+ * without attentive pooling and tdnn models, VOX_BF16; other plans (dpn68, the
+ * attentive models, fp32) return VOX_EINVAL.
  * _device: d_lens is a device int32 [n] array (read in stream order);
  * vox_embed_lens: host buffers, lens checked on the host. */
 int vox_embed_device_lens(vox_model* m, const float* d_x, int n, int t, int f,

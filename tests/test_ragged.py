@@ -93,8 +93,9 @@ def test_ragged_unsupported_plans_refuse(weights):
     from voxsrc2020_speaker_verification_amd._native import VoxError
     from voxsrc2020_speaker_verification_amd.extractor import Extractor
     x = np.zeros((2, 64, 80), np.float32)
-    spec, t, blob = weights("tdnn", 80)
+    spec, t, blob = weights("dpn68", 80)
     with Extractor(blob, precision="bf16") as ex:
+        assert not ex.supports_lengths()
         with pytest.raises(VoxError):
             ex.run_lens(x, [64, 40])
         ex.run(x)                                   # the handle still works
@@ -128,6 +129,23 @@ def test_ragged_other_res2nets(weights, name, F):
             with pytest.raises(VoxError):
                 ex.run_lens(x, lens)
             return
+        got = ex.run_lens(x, lens)
+        exp = _exact(ex, x, lens)
+        bad = [lens[i] for i in range(len(lens)) if not np.array_equal(got[i], exp[i])]
+        assert not bad, bad
+
+
+@pytest.mark.parametrize("F,T,lens", [(80, 200, [200, 199, 150, 64, 33, 25]),
+                                      (40, 320, [320, 301, 256, 100, 25, 26])])
+def test_ragged_tdnn_bitwise_equal_exact_runs(weights, F, T, lens):
+    """TDNN (C1 / C2 geometries): the dilated layers' tap gather
+    (gemm1x1_ws<.., GS_TAPS>) reads the rows past an utterance's frames as its
+    SAME padding; every row equals its exact run."""
+    from voxsrc2020_speaker_verification_amd.extractor import Extractor
+    spec, t, blob = weights("tdnn", F)
+    x = _batch(lens, T, F, np.random.default_rng(F + T))
+    with Extractor(blob, precision="bf16") as ex:
+        assert ex.supports_lengths()
         got = ex.run_lens(x, lens)
         exp = _exact(ex, x, lens)
         bad = [lens[i] for i in range(len(lens)) if not np.array_equal(got[i], exp[i])]

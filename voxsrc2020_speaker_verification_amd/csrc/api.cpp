@@ -1759,7 +1759,11 @@ static bool ragged_ok(const Op& op, DType dt) {
       return true;
     case 3: return op.C % 8 == 0 && op.lds % 8 == 0 && op.ldd % 8 == 0;   // avgpool3s2_v8
     case 5: return op.kind == OP_HEAD;             // the fp32 head dense
-    case 21: case 9: case 18: case 29: case 8:     // 1x1 convs (per pixel)
+    case 21:                                       // 1x1 (per pixel) or the TDNN's taps
+      if (op.cp.kh > 1)                            // GS_TAPS: the tap rows masked (gemm_wide.hip)
+        return op.cp.kw == 1 && op.cp.W == 1 && op.cp.wblk && !op.cp.in_mean && !op.cp.res;
+      return op.cp.kw == 1 && !op.cp.in_mean;
+    case 9: case 18: case 29: case 8:              // 1x1 convs (per pixel)
       return op.cp.kh == 1 && op.cp.kw == 1 && !op.cp.in_mean;
   }
   return false;
@@ -1771,8 +1775,9 @@ static int build_plan(vox_model* m, const float* x, int n, int t, float* out, bo
     m->plan.clear();
     m->taps.clear();
     if (rag) {
-      if (m->family != "res2net" || m->att)
-        return fail(VOX_EINVAL, "per-utterance lengths: res2net models without attentive pooling only");
+      if ((m->family != "res2net" && m->family != "tdnn") || m->att)
+        return fail(VOX_EINVAL, "per-utterance lengths: res2net (without attentive pooling) and "
+                                "tdnn models only");
       B.vlen = (const int*)B.base(S_LEN, (size_t)n * 4);
     }
     if (m->family == "tdnn") return build_tdnn(B, x, n, t, out);

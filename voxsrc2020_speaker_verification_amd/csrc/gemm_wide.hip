@@ -510,6 +510,7 @@ __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
     const int wstep = blk ? 512 : 32;   // elements per k-step of a weight piece
     int l_tile = 0, l_k = 0, l_co0 = 0, l_px0 = 0;
     int tho[NLL];   // GS_TAPS: the B row's time index (its utterance base is in src)
+    int thn[NLL];   // GS_TAPS: its utterance's valid rows (ragged batches; H otherwise)
     const bf16_t* zero = reinterpret_cast<const bf16_t*>(g_gw_zero);
     auto set_load_tile = [&](int tj) {
       const int lid = t_first + tj * t_step;
@@ -532,6 +533,7 @@ __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
           if constexpr (TAPS) {
             src[i] = X + (size_t)n * p.H * p.ldx + c * 8;   // W = 1: row h at h * ldx
             tho[i] = ho;
+            thn[i] = valid_rows(p.vlen, p.vsh, n, p.H);
           } else {
             src[i] = X + (((size_t)n * p.H + ho * p.sh) * p.W + wo * p.sw) * p.ldx + c * 8;
           }
@@ -563,7 +565,7 @@ __global__ __launch_bounds__(GS_NT) void gemm1x1_ws(ConvParams p) {
             const bf16_t* a = src[i] + kk * kst;
             if (TAPS && i >= BN / 64) {
               const int hi = tho[i] + sh_t;
-              a = (hi >= 0 && hi < p.H) ? src[i] + (size_t)hi * p.ldx + ci0 : zero;
+              a = (hi >= 0 && hi < thn[i]) ? src[i] + (size_t)hi * p.ldx + ci0 : zero;
             }
             if ((DBG & 2048) && i >= BN / 64)   // (diagnostics: activation pieces nt)
               gw_glds16_nt(a, lds0 + (uint32_t)slot * SLOTB + (uint32_t)(u * SUBB) + (uint32_t)gi * 1024u);
