@@ -1025,7 +1025,8 @@ static void emit_head(Builder& B, const float* pooled, int n, float* out) {
   B.ops->push_back(r);
 }
 
-static const void* emit_input(Builder& B, const float* x, int64_t count) {
+// H / rowlen: the batch's rows (ragged batches zero each utterance's padded rows)
+static const void* emit_input(Builder& B, const float* x, int64_t count, int H = 1, int rowlen = 1) {
   vox_model* m = B.m;
   if (m->dt == F32) return x;
   void* in = B.base(S_IN, (size_t)count * 2);
@@ -1033,6 +1034,7 @@ static const void* emit_input(Builder& B, const float* x, int64_t count) {
   op.kind = OP_OTHER;
   op.type = 4;
   op.src = x; op.dst = in; op.count = count;
+  op.vlen = B.vlen; op.H = H; op.W = rowlen;
   op.bytes = 6.0 * count;
   B.ops->push_back(op);
   return in;
@@ -1054,7 +1056,7 @@ static void emit_stem(Builder& B, const ConvW& stem, const float* x, int n, int 
     B.ops->push_back(op);
     return;
   }
-  Act in{emit_input(B, x, (int64_t)n * H * W), 1, n, H, W, 1};
+  Act in{emit_input(B, x, (int64_t)n * H * W, H, W), 1, n, H, W, 1};
   emit_conv(B, stem, in, nullptr, 0, 1, 1, 1, 1, 1, 1, H, W, y, stem.cout, EPI_AFFINE | EPI_RELU);
 }
 
@@ -1086,7 +1088,7 @@ static int build_tdnn(Builder& B, const float* x, int n, int t, float* out) {
   const size_t es = es_of(m);
   auto kern = m->spec.getv("kernels");
   auto dil = m->spec.getv("dilations");
-  Act a{emit_input(B, x, (int64_t)n * t * F), F, n, t, 1, F};
+  Act a{emit_input(B, x, (int64_t)n * t * F, t, F), F, n, t, 1, F};
   Slot ping[2] = {S_X0, S_X1};
   for (size_t l = 0; l < m->convs.size(); ++l) {
     const ConvW& cw = m->convs[l];
@@ -1874,7 +1876,8 @@ static hipError_t run_op(vox_model* m, const Op& op, hipStream_t s) {
     case 3:
       return launch_avgpool3s2(m->dt, op.src, op.lds, op.N, op.H, op.W, op.C, op.dst, op.ldd, op.Ho,
                                op.Wo, s, op.vlen, op.vsh);
-    case 4: return launch_convert_f32(m->dt, (const float*)op.src, op.dst, op.count, s);
+    case 4: return launch_convert_f32(m->dt, (const float*)op.src, op.dst, op.count, s, op.vlen,
+                                      op.H, op.W);
     case 6:
       return launch_bnrelu_inplace(m->dt, op.dst, op.ldd, (int64_t)op.N * op.H * op.W, op.C,
                                    op.mean, op.inv, s);

@@ -282,7 +282,9 @@ hipError_t launch_avgpool3s2(DType t, const void* x, int ldx, int N, int H, int 
                              void* y, int ldy, int Ho, int Wo, hipStream_t s,
                              const int* vlen = nullptr, int vsh = 0);
 
-hipError_t launch_convert_f32(DType t, const float* x, void* y, int64_t n, hipStream_t s);
+// vlen (ragged batches, n = N * H * rowlen): rows past an utterance's frames -> 0
+hipError_t launch_convert_f32(DType t, const float* x, void* y, int64_t n, hipStream_t s,
+                              const int* vlen = nullptr, int H = 1, int rowlen = 1);
 
 hipError_t launch_copy_channels(DType t, const void* x, int ldx, void* y, int ldy,
                                 int64_t npix, int C, hipStream_t s);

@@ -1878,15 +1878,31 @@ hipError_t launch_avgpool3s2(DType t, const void* x, int ldx, int N, int H, int 
 }
 
 // ----------------------------------------------------------------------------
-__global__ void convert_f32_bf16(const float* __restrict__ x, bf16_t* __restrict__ y, int64_t n) {
+// vlen (ragged batches): n = N * H * rowlen elements; the rows of utterance u
+// past its vlen[u] frames are written as zeros -- a kernel whose K is padded
+// past a row's channels (the TDNN's first layer: 80 of 96) reads the start of
+// the next row against zero weights, and NaN padding times zero is NaN
+__global__ void convert_f32_bf16(const float* __restrict__ x, bf16_t* __restrict__ y, int64_t n,
+                                 const int* __restrict__ vlen, int H, int rowlen) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) y[i] = (bf16_t)x[i];
+  if (i >= n) return;
+  float v = x[i];
+  if (vlen) {
+    const int64_t r = i / rowlen;              // row over the batch
+    const int u = (int)(r / H), h = (int)(r - (int64_t)u * H);
+    if (h >= vlen[u]) v = 0.f;
+  }
+  y[i] = (bf16_t)v;
 }
 
-hipError_t launch_convert_f32(DType t, const float* x, void* y, int64_t n, hipStream_t s) {
-  if (t == F32) return hipMemcpyAsync(y, x, n * 4, hipMemcpyDeviceToDevice, s);
+hipError_t launch_convert_f32(DType t, const float* x, void* y, int64_t n, hipStream_t s,
+                              const int* vlen, int H, int rowlen) {
+  if (t == F32) {
+    if (vlen) return hipErrorInvalidValue;   // ragged batches run bf16 plans only
+    return hipMemcpyAsync(y, x, n * 4, hipMemcpyDeviceToDevice, s);
+  }
   hipLaunchKernelGGL(convert_f32_bf16, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x,
-                     (bf16_t*)y, n);
+                     (bf16_t*)y, n, vlen, H, rowlen);
   return hipGetLastError();
 }
 
