@@ -31,7 +31,7 @@ SOURCES = [
     ("gemm_nw.hip", ["-O3"]),
     ("fbank.hip", ["-O3"]),
     ("api.cpp", ["-O2"]),
-    ("kaldi_host.cpp", ["-O2", "-ffp-contract=off"]),
+    ("kaldi_host.cpp", ["-O2", "-ffp-contract=off", "--offload-host-only"]),
 ]
 
 

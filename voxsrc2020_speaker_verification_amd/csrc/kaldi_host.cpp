@@ -14,8 +14,11 @@
 // Compiled with -ffp-contract=off so no multiply-add is fused.
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
 #include <cstdio>
 #include <cstring>
+#include <functional>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -28,10 +31,13 @@ static int kfail(int code, const char* msg) { return vox_set_error(code, msg); }
 // The recursion over t in [0, t1) (the running sums always start at t = 0, so
 // every output row has the same bits as the whole-utterance pass); rows
 // t >= t0 are written to out[(t - t0) * F].
-static void sliding_cmn_rows(const float* in, int T, int F, int cmn_window, int center, int t0,
-                             int t1, float* out) {
+// (cloned for AVX2 with a run-time pick: the loops are element-wise over F,
+// nothing is reassociated or contracted, so every clone gives the same bits)
+__attribute__((target_clones("avx2", "default")))
+static void sliding_cmn_kernel(const float* in, int T, int F, int cmn_window, int center, int t0,
+                               int t1, float* out, double* sum) {
   const int min_window = 100;  // Kaldi default (only used when center == false)
-  std::vector<double> sum(F, 0.0);
+  for (int f = 0; f < F; ++f) sum[f] = 0.0;
   int last_start = -1, last_end = -1;
   for (int t = 0; t < t1; ++t) {
     int ws, we;
@@ -69,6 +75,13 @@ static void sliding_cmn_rows(const float* in, int T, int F, int cmn_window, int 
     for (int f = 0; f < F; ++f)
       out[(size_t)(t - t0) * F + f] = (float)((double)in[(size_t)t * F + f] + alpha * sum[f]);
   }
+}
+
+static void sliding_cmn_rows(const float* in, int T, int F, int cmn_window, int center, int t0,
+                             int t1, float* out) {
+  thread_local std::vector<double> sum;
+  sum.resize(F);
+  sliding_cmn_kernel(in, T, F, cmn_window, center, t0, t1, out, sum.data());
 }
 
 extern "C" int vox_sliding_cmn(const float* in, int T, int F, int cmn_window, int center,
@@ -160,15 +173,27 @@ int parse_payload(Reader& r, int kind, int rows, int cols, float* out, int cm_ka
     for (size_t i = 0; i < n; ++i) out[i] = mn + (float)q[i] * inc;
     return VOX_OK;
   }
-  std::vector<uint16_t> ch((size_t)cols * 4);
-  if (!r.take(ch.data(), ch.size() * 2)) return kfail(VOX_EIO, "truncated CM column headers");
-  std::vector<uint8_t> data(n);
-  if (!r.take(data.data(), n)) return kfail(VOX_EIO, "truncated CM payload");
+  // column headers and bytes are decoded in place (no copy of the payload)
+  const size_t nch = (size_t)cols * 8;
+  if (nch > r.n - r.i) return kfail(VOX_EIO, "truncated CM column headers");
+  const uint8_t* ch = r.p + r.i;
+  r.i += nch;
+  if (n > r.n - r.i) return kfail(VOX_EIO, "truncated CM payload");
+  const uint8_t* data = r.p + r.i;
+  r.i += n;
   const float c = 1.52590218966964e-05f;
+  // Each column maps its 256 byte codes through 4 percentiles, so the decode
+  // is a per-column table of the 256 values (each computed by the formula
+  // below, so the same bits) and the payload pass is a lookup, written row by
+  // row: 256 * cols formula evaluations instead of rows * cols branchy ones.
+  thread_local std::vector<float> lut;
+  lut.resize((size_t)cols * 256);
   for (int col = 0; col < cols; ++col) {
     float p[4];
     for (int k = 0; k < 4; ++k) {
-      const float u = (float)ch[(size_t)col * 4 + k];
+      uint16_t hv;
+      std::memcpy(&hv, ch + ((size_t)col * 4 + k) * 2, 2);
+      const float u = (float)hv;
       if (cm_kaldi) {
         p[k] = mn + (range * c) * u;
       } else {
@@ -178,29 +203,29 @@ int parse_payload(Reader& r, int kind, int rows, int cols, float* out, int cm_ka
         p[k] = v + mn;
       }
     }
-    const uint8_t* d = data.data() + (size_t)col * rows;  // column-major
+    float* L = &lut[(size_t)col * 256];
     if (cm_kaldi) {
-      for (int row = 0; row < rows; ++row) {
-        const unsigned v = d[row];
-        double x;
-        if (v <= 64) x = (double)p[0] + (double)((p[1] - p[0]) * (float)v) * (1 / 64.0);
-        else if (v <= 192) x = (double)p[1] + (double)((p[2] - p[1]) * (float)(v - 64)) * (1 / 128.0);
-        else x = (double)p[2] + (double)((p[3] - p[2]) * (float)(v - 192)) * (1 / 63.0);
-        out[(size_t)row * cols + col] = (float)x;
-      }
+      // the three segments as branch-free loops (v <= 64, <= 192, above)
+      for (int v = 0; v <= 64; ++v)
+        L[v] = (float)((double)p[0] + (double)((p[1] - p[0]) * (float)v) * (1 / 64.0));
+      for (int v = 65; v <= 192; ++v)
+        L[v] = (float)((double)p[1] + (double)((p[2] - p[1]) * (float)(v - 64)) * (1 / 128.0));
+      for (int v = 193; v < 256; ++v)
+        L[v] = (float)((double)p[2] + (double)((p[3] - p[2]) * (float)(v - 192)) * (1 / 63.0));
       continue;
     }
     const float s0 = (p[1] - p[0]) / 64.0f;
     const float s1 = (p[2] - p[1]) / 128.0f;
     const float s2 = (p[3] - p[2]) / 63.0f;
-    for (int row = 0; row < rows; ++row) {
-      const unsigned v = d[row];
-      float x;
-      if (v <= 64) x = p[0] + s0 * (float)v;
-      else if (v <= 192) x = p[1] + s1 * (float)(v - 64);
-      else x = p[2] + s2 * (float)(v - 192);
-      out[(size_t)row * cols + col] = x;
-    }
+    for (int v = 0; v <= 64; ++v) L[v] = p[0] + s0 * (float)v;
+    for (int v = 65; v <= 192; ++v) L[v] = p[1] + s1 * (float)(v - 64);
+    for (int v = 193; v < 256; ++v) L[v] = p[2] + s2 * (float)(v - 192);
+  }
+  // payload is column-major (rows bytes per column); out is row-major
+  for (int row = 0; row < rows; ++row) {
+    float* o = out + (size_t)row * cols;
+    const uint8_t* d = data + row;
+    for (int col = 0; col < cols; ++col) o[col] = lut[(size_t)col * 256 + d[(size_t)col * rows]];
   }
   return VOX_OK;
 }
@@ -349,10 +374,74 @@ struct FirstError {
 };
 
 // body(i) for i < n on up to `threads` workers (the caller is one of them).
-// Nothing escapes to the extern "C" callers: an exception in a body (e.g.
-// std::bad_alloc) stops the loop and is returned as VOX_EIO, and a worker
-// thread that cannot be started leaves its share to the ones that did
-// (down to the calling thread alone).
+// The workers are persistent: each calling thread (an extraction lane, the
+// main thread) owns a pool that grows to the largest `threads` it asked for
+// and is joined when that thread exits, so the workers' thread_local decode
+// buffers stay mapped across calls (a fresh thread per call re-faulted them
+// every batch, which cost more than the decode itself).  Nothing escapes to
+// the extern "C" callers: an exception in a body (e.g. std::bad_alloc) stops
+// the loop and is returned as VOX_EIO, and a worker that cannot be started
+// leaves its share to the ones that did (down to the calling thread alone).
+class WorkerPool {
+ public:
+  ~WorkerPool() {
+    {
+      std::lock_guard<std::mutex> l(m_);
+      stop_ = true;
+    }
+    go_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  // runs job() on the caller and on min(want, size) - 1 workers; returns when all are done
+  void run(int want, const std::function<void()>& job) {
+    grow(want - 1);
+    std::unique_lock<std::mutex> l(m_);
+    job_ = &job;
+    active_ = std::min<int>(want - 1, (int)th_.size());
+    helpers_ = active_;
+    ++gen_;
+    l.unlock();
+    go_.notify_all();
+    job();
+    l.lock();
+    done_.wait(l, [&] { return active_ == 0; });
+    job_ = nullptr;
+  }
+
+ private:
+  void grow(int k) {
+    try {
+      while ((int)th_.size() < k) {
+        const int idx = (int)th_.size();
+        th_.emplace_back([this, idx] { loop(idx); });
+      }
+    } catch (...) {
+      // std::system_error / bad_alloc: run with the workers already started
+    }
+  }
+  void loop(int idx) {
+    uint64_t seen = 0;
+    std::unique_lock<std::mutex> l(m_);
+    for (;;) {
+      go_.wait(l, [&] { return stop_ || (gen_ != seen && idx < helpers_); });
+      if (stop_) return;
+      seen = gen_;
+      const std::function<void()>* j = job_;
+      l.unlock();
+      (*j)();
+      l.lock();
+      if (--active_ == 0) done_.notify_one();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex m_;
+  std::condition_variable go_, done_;
+  const std::function<void()>* job_ = nullptr;
+  uint64_t gen_ = 0;
+  int active_ = 0, helpers_ = 0;
+  bool stop_ = false;
+};
+
 template <typename F>
 int parallel_for(int n, int threads, F&& body) noexcept {
   threads = std::max(1, std::min(threads, n));
@@ -366,15 +455,17 @@ int parallel_for(int n, int threads, F&& body) noexcept {
       next.store(n);
     }
   };
-  std::vector<std::thread> pool;
-  try {
-    pool.reserve(threads - 1);
-    for (int k = 1; k < threads; ++k) pool.emplace_back(work);
-  } catch (...) {
-    // std::system_error / bad_alloc: run with the workers already started
+  if (threads == 1) {
+    work();
+  } else {
+    try {
+      static thread_local WorkerPool pool;
+      const std::function<void()> job = work;
+      pool.run(threads, job);
+    } catch (...) {
+      work();   // no pool (allocation failed): the calling thread alone
+    }
   }
-  work();
-  for (auto& t : pool) t.join();
   if (threw.load()) {
     try {
       return kfail(VOX_EIO, "host worker failed (out of memory?)");
