@@ -18,9 +18,10 @@ into a Queue(32), and the session runs each <= 1000-frame chunk on its own
      pinned host buffer by the native reader (`vox_read_chunks`, host threads)
      while the lane's previous batch runs on the GPU;
   3. compute: the batches go round-robin to `lanes` extraction handles, each
-     driven by its own host thread with its own stream, device buffers and
-     resident plans; the H2D copy, the forward and the D2H copy of one batch
-     are queued on its lane's stream.
+     driven by its own host thread with its own streams, device buffers and
+     resident plans; a batch's H2D copy is queued on the lane's copy stream
+     (overlapping the previous forward), its forward and D2H copy on the
+     lane's compute stream.
 
 Host memory is two batches of features per lane plus one embedding per
 utterance; nothing grows with the features of the shard.  The per-utterance
@@ -32,6 +33,8 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import threading
+import time
 
 import numpy as np
 
@@ -183,31 +186,66 @@ def plan_batches(lengths, batch, keys=None, ragged=False):
 
 class Combiner:
     """Per-utterance length-weighted mean of its chunk embeddings in chunk
-    order (extract.embed_utterances' float32 arithmetic, tf_extract.py:108-111);
-    multi-chunk utterances wait here until their last chunk arrives."""
+    order (extract.embed_utterances' float32 arithmetic, tf_extract.py:108-111:
+    acc = 0; acc = acc + e_c * L_c; acc / sum L), a batch at a time in numpy:
+    single-chunk utterances are finished with the batch; the rows of
+    multi-chunk ones wait in one array and an utterance is finished, with the
+    others of its chunk count, in the batch that brings its last chunk.  The
+    operations are the scalar loop's, element-wise in float32, so the bits are
+    the same."""
 
     def __init__(self, plans, dim):
         self.plans = plans
         self.out = np.empty((len(plans), dim), np.float32)
-        self._part = {}
         self.done = 0
+        nch = np.fromiter((len(p) for p in plans), np.int64, len(plans))
+        self._nch = nch
+        self._left = nch.copy()
+        # rows of multi-chunk utterances: slot base[u] + ci
+        multi = nch > 1
+        base = np.full(len(plans), -1, np.int64)
+        base[multi] = np.concatenate([[0], np.cumsum(nch[multi])[:-1]]) if multi.any() else []
+        self._base = base
+        self._pend = np.empty((int(nch[multi].sum()), dim), np.float32)
+        kmax = int(nch.max()) if len(plans) else 1
+        self._lens = np.zeros((len(plans), kmax), np.float32)     # chunk lengths
+        for k, p in enumerate(plans):
+            self._lens[k, :len(p)] = [L for _, L in p]
+        self._tot = self._lens.sum(axis=1, keepdims=True)         # exact: integers < 2^24
+
+    def add_batch(self, items, rows):
+        """items [(u, ci, start)] of one batch, rows [n, dim] float32."""
+        rows = np.asarray(rows, np.float32)
+        uc = np.array([it[:2] for it in items], np.int64).reshape(-1, 2)
+        u, ci = uc[:, 0], uc[:, 1]
+        one = self._nch[u] == 1
+        if one.all():
+            L = self._lens[u, :1]
+            self.out[u] = (np.float32(0) + rows * L) / L
+            self.done += len(u)
+            return
+        if one.any():
+            us = u[one]
+            L = self._lens[us, :1]
+            self.out[us] = (np.float32(0) + rows[one] * L) / L
+            self.done += len(us)
+        mu, mc = u[~one], ci[~one]
+        self._pend[self._base[mu] + mc] = rows[~one]
+        np.subtract.at(self._left, mu, 1)
+        fin = np.unique(mu[self._left[mu] == 0])
+        if not len(fin):
+            return
+        for k in np.unique(self._nch[fin]):
+            us = fin[self._nch[fin] == k]
+            lens, b0 = self._lens[us], self._base[us]
+            acc = np.float32(0) + self._pend[b0] * lens[:, :1]
+            for c in range(1, int(k)):
+                acc = acc + self._pend[b0 + c] * lens[:, c:c + 1]
+            self.out[us] = acc / self._tot[us]
+            self.done += len(us)
 
     def add(self, u, ci, row):
-        plan = self.plans[u]
-        if len(plan) == 1:
-            rows = [row]
-        else:
-            got = self._part.setdefault(u, {})
-            got[ci] = row
-            if len(got) < len(plan):
-                return
-            rows = [got[i] for i in range(len(plan))]
-            del self._part[u]
-        acc = 0
-        for r, (_, L) in zip(rows, plan):
-            acc = acc + r * L
-        self.out[u] = acc / sum(L for _, L in plan)
-        self.done += 1
+        self.add_batch([(u, ci, 0)], np.asarray(row, np.float32)[None])
 
 
 class SyncRunner:
@@ -229,9 +267,11 @@ class LanePool:
     thread: lane k takes batches k, k + K, k + 2K, ...; for each it reads the
     chunks into one of its two pinned buffers with the native reader (the
     GIL is released in every native call, so the lanes' reading, planning and
-    launching run in parallel), queues H2D + forward + D2H on its stream, and
-    then finishes its previous batch -- so every lane keeps two batches in
-    flight and the host work of one hides behind the GPU work of the other."""
+    launching run in parallel), queues the H2D on its copy stream (into one of
+    two device buffers) and the forward + D2H on its compute stream, and then
+    finishes its previous batch -- so every lane keeps two batches in flight,
+    the host work of one hides behind the GPU work of the other, and a batch's
+    PCIe transfer overlaps the previous batch's forward."""
 
     def __init__(self, extractors, table, batches, cmn=True):
         import torch
@@ -244,23 +284,38 @@ class LanePool:
         max_n = max((len(b[1]) for b in batches), default=1)
         # ragged batches (L, items, lens): per-lane device lengths + pinned copies
         self.ragged = bool(batches) and len(batches[0]) == 3
-        self.d_len = [torch.empty(max_n, dtype=torch.int32, device=self.dev) for _ in range(K)]
+        self.d_len = [[torch.empty(max_n, dtype=torch.int32, device=self.dev) for _ in range(2)]
+                      for _ in range(K)]
         self.h_len = [[torch.empty(max_n, dtype=torch.int32).pin_memory() for _ in range(2)]
                       for _ in range(K)]
         self.threads = max(1, table.threads // K)
         self.streams = [torch.cuda.Stream(self.dev) for _ in range(K)]
+        # H2D copies on a stream of their own per lane, into two staging buffers,
+        # so batch i+1's features cross PCIe while batch i computes (a fast
+        # model -- the TDNN at ~1e8 frames/s -- reads ~30 GB/s of float32
+        # features); the compute stream moves a batch from its staging buffer
+        # into the lane's one input buffer (a D2D copy, microseconds), so the
+        # resident plans, keyed on the input address, stay one per shape
+        self.copy_streams = [torch.cuda.Stream(self.dev) for _ in range(K)]
+        self.d_stage = [[torch.empty(max_el, dtype=torch.float32, device=self.dev)
+                         for _ in range(2)] for _ in range(K)]
         self.d_in = [torch.empty(max_el, dtype=torch.float32, device=self.dev) for _ in range(K)]
         self.d_out = [torch.empty(max_n * dim, dtype=torch.float32, device=self.dev) for _ in range(K)]
         self.h_in = [[torch.empty(max_el, dtype=torch.float32).pin_memory() for _ in range(2)]
                      for _ in range(K)]
         self.h_out = [[torch.empty(max_n * dim, dtype=torch.float32).pin_memory() for _ in range(2)]
                       for _ in range(K)]
+        # host seconds per phase, summed over the lanes (tools/bench_extract.py)
+        self.phase = {"read": 0.0, "launch": 0.0, "wait": 0.0}
+        self._lock = threading.Lock()
 
     def _lane(self, k, batches, results, stop):
-        torch, ex, s = self.torch, self.exs[k], self.streams[k]
+        torch, ex, s, cs = self.torch, self.exs[k], self.streams[k], self.copy_streams[k]
         F, dim = self.table.feat_dim, ex.dim
-        prev = None            # (bid, n, done event, pinned output)
-        free = [None, None]    # event after the H2D that last read h_in[k][j]
+        prev = None              # (bid, n, done event, pinned output)
+        free = [None, None]      # event after the H2D that last read h_in[k][j]
+        used = [None, None]      # event after the D2D that last read d_stage[k][j]
+        clock, ph = time.perf_counter, {"read": 0.0, "launch": 0.0, "wait": 0.0}
         try:
             torch.cuda.set_device(self.dev)
             for i, b in enumerate(range(k, len(batches), len(self.exs))):
@@ -268,8 +323,10 @@ class LanePool:
                     return
                 L, items = batches[b][0], batches[b][1]
                 n, j = len(items), i & 1
+                t0 = clock()
                 if free[j] is not None:
                     free[j].synchronize()
+                t1 = clock()
                 hin = self.h_in[k][j]
                 if self.ragged:
                     lens = batches[b][2]
@@ -278,14 +335,22 @@ class LanePool:
                     hl[:n].copy_(torch.tensor(lens, dtype=torch.int32))
                 else:
                     self.table.read(items, L, hin, self.cmn, self.threads)
-                x, o = self.d_in[k][:n * L * F], self.d_out[k][:n * dim]
-                dl = self.d_len[k][:n]
-                with torch.cuda.stream(s):
-                    x.copy_(hin[:n * L * F], non_blocking=True)
+                t2 = clock()
+                xs, x = self.d_stage[k][j][:n * L * F], self.d_in[k][:n * L * F]
+                o, dl = self.d_out[k][:n * dim], self.d_len[k][j][:n]
+                with torch.cuda.stream(cs):
+                    if used[j] is not None:
+                        cs.wait_event(used[j])
+                    xs.copy_(hin[:n * L * F], non_blocking=True)
                     if self.ragged:
                         dl.copy_(hl[:n], non_blocking=True)
                     free[j] = torch.cuda.Event()
-                    free[j].record(s)
+                    free[j].record(cs)
+                s.wait_event(free[j])
+                with torch.cuda.stream(s):
+                    x.copy_(xs)
+                    used[j] = torch.cuda.Event()
+                    used[j].record(s)
                 if self.ragged:
                     ex.run_device_lens(x.view(n, L, F), dl, o.view(n, dim), s)
                 else:
@@ -295,14 +360,21 @@ class LanePool:
                     h[:n * dim].copy_(o, non_blocking=True)
                     done = torch.cuda.Event()
                     done.record(s)
+                t3 = clock()
                 if prev is not None:
                     results.put(self._finish(prev, dim))
                 prev = (b, n, done, h)
+                ph["wait"] += clock() - t3 + t1 - t0
+                ph["read"] += t2 - t1
+                ph["launch"] += t3 - t2
             if prev is not None:
                 results.put(self._finish(prev, dim))
         except BaseException as e:   # surfaced by run() on the consuming thread
             results.put(e)
         finally:
+            with self._lock:
+                for key, v in ph.items():
+                    self.phase[key] += v
             results.put(None)
 
     @staticmethod
@@ -313,7 +385,6 @@ class LanePool:
 
     def run(self, batches):
         import queue
-        import threading
         results, stop = queue.Queue(), []
         lanes = [threading.Thread(target=self._lane, args=(k, batches, results, stop), daemon=True)
                  for k in range(len(self.exs))]
@@ -338,7 +409,7 @@ class LanePool:
             # abandoning the generator) may have left its last batch queued: the
             # H2D from its pinned buffer, the forward and the D2H still run on
             # its stream.  Drain them before the buffers can be freed or reused
-            for s in self.streams:
+            for s in self.streams + self.copy_streams:
                 s.synchronize()
         if err is not None:
             raise err
@@ -354,8 +425,7 @@ def extract_stream(table, make_runner, batch=64, ragged=False):
     for bid, rows in make_runner(batches).run(batches):
         if comb is None:
             comb = Combiner(plans, rows.shape[1])
-        for (u, ci, _), row in zip(batches[bid][1], rows):
-            comb.add(u, ci, row)
+        comb.add_batch(batches[bid][1], rows)
     if comb is None:
         return list(table.keys), None
     assert comb.done == len(plans), (comb.done, len(plans))
