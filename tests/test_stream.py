@@ -172,3 +172,31 @@ def test_ragged_reader_and_stream(shard):
     keys, got = extract_stream(table, Runner, 4, ragged=True)
     keys2, ref = extract.extract_scp(shard, _embed, 80, 4, threads=3)
     assert keys == keys2 and np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("ragged", [True, False])
+def test_combiner_batches_match_the_scalar_loop(ragged):
+    """Combiner.add_batch (numpy over a batch) gives the bits of
+    embed_utterances' per-utterance loop (acc = 0; acc = acc + e * L; acc /
+    sum L, float32), chunks arriving in any batch order, signed zeros kept as
+    that loop keeps them."""
+    from voxsrc2020_speaker_verification_amd import stream
+    rng = np.random.default_rng(5)
+    T = rng.integers(25, 3501, 700)
+    T[:6] = [25, 1000, 1001, 2000, 3499, 999]
+    plans, batches = stream.plan_batches(T, 64, ragged=ragged)
+    order = rng.permutation(len(batches))
+    rows = [rng.standard_normal((len(b[1]), 16)).astype(np.float32) for b in batches]
+    rows[0][0, :4] = [-0.0, 0.0, 1e-30, -1e-30]
+    comb = stream.Combiner(plans, 16)
+    for i in order:
+        comb.add_batch(batches[i][1], rows[i])
+    assert comb.done == len(plans)
+    emb = {(u, ci): r for b, rr in zip(batches, rows) for (u, ci, _), r in zip(b[1], rr)}
+    ref = np.empty_like(comb.out)
+    for u, plan in enumerate(plans):
+        acc = 0
+        for ci, (_, L) in enumerate(plan):
+            acc = acc + emb[(u, ci)] * L
+        ref[u] = acc / sum(L for _, L in plan)
+    assert np.array_equal(ref.view(np.uint32), comb.out.view(np.uint32))
