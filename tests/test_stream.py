@@ -200,3 +200,45 @@ def test_combiner_batches_match_the_scalar_loop(ragged):
             acc = acc + emb[(u, ci)] * L
         ref[u] = acc / sum(L for _, L in plan)
     assert np.array_equal(ref.view(np.uint32), comb.out.view(np.uint32))
+
+
+def test_reader_pool_concurrent_lanes_match_one_thread(tmp_path):
+    """The native reader's persistent worker pools (one per calling thread):
+    four Python threads reading ragged batches at once, each asking for a
+    different worker count, get the bytes of a one-thread read."""
+    import threading
+    from voxsrc2020_speaker_verification_amd import kaldi, stream
+    rng = np.random.default_rng(11)
+    ark, scp = str(tmp_path / "f.ark"), str(tmp_path / "f.scp")
+    with open(ark, "wb") as fa, open(scp, "w") as fs:
+        for i in range(96):
+            rec, off = kaldi.format_mat_flt(f"u{i}", rng.standard_normal(
+                (int(rng.integers(30, 1400)), 24)).astype(np.float32))
+            pos = fa.tell()
+            fa.write(rec)
+            fs.write(f"u{i} {ark}:{pos + off}\n")
+    table = stream.ChunkTable(kaldi.read_scp(scp), threads=4)
+    _, batches = stream.plan_batches(table.T, 16, ragged=True)
+    size = 16 * stream.MAX_FRAMES * 24
+    ref = []
+    for Lp, items, lens in batches:
+        b = np.zeros(size, np.float32)
+        table.read_ragged(items, lens, Lp, b, threads=1)
+        ref.append(b)
+    bad = []
+
+    def lane(k):
+        for _ in range(3):
+            for j in range(k, len(batches), 4):
+                Lp, items, lens = batches[j]
+                b = np.zeros(size, np.float32)
+                table.read_ragged(items, lens, Lp, b, threads=2 + k)
+                if not np.array_equal(b, ref[j]):
+                    bad.append(j)
+
+    ts = [threading.Thread(target=lane, args=(k,)) for k in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not bad
