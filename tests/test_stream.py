@@ -242,3 +242,44 @@ def test_reader_pool_concurrent_lanes_match_one_thread(tmp_path):
     for t in ts:
         t.join()
     assert not bad
+
+
+def _read_in_child(scp, q):
+    from voxsrc2020_speaker_verification_amd import kaldi, stream
+    table = stream.ChunkTable(kaldi.read_scp(scp), threads=4)
+    _, batches = stream.plan_batches(table.T, 16, ragged=True)
+    Lp, items, lens = batches[0]
+    b = np.zeros(16 * Lp * table.feat_dim, np.float32)
+    table.read_ragged(items, lens, Lp, b)
+    q.put(float(np.abs(b).sum()))
+
+
+def test_reader_pool_after_fork(tmp_path):
+    """A process forked after the reader's worker pool exists (multiprocessing's
+    fork start method) reads with a pool of its own instead of waiting on the
+    parent's threads, which the child does not have."""
+    import multiprocessing as mp
+    from voxsrc2020_speaker_verification_amd import kaldi, stream
+    rng = np.random.default_rng(12)
+    ark, scp = str(tmp_path / "f.ark"), str(tmp_path / "f.scp")
+    with open(ark, "wb") as fa, open(scp, "w") as fs:
+        for i in range(20):
+            rec, off = kaldi.format_mat_flt(f"u{i}", rng.standard_normal((300 + 7 * i, 8)).astype(np.float32))
+            pos = fa.tell()
+            fa.write(rec)
+            fs.write(f"u{i} {ark}:{pos + off}\n")
+    table = stream.ChunkTable(kaldi.read_scp(scp), threads=4)
+    _, batches = stream.plan_batches(table.T, 16, ragged=True)
+    Lp, items, lens = batches[0]
+    b = np.zeros(16 * Lp * 8, np.float32)
+    table.read_ragged(items, lens, Lp, b)              # the parent's pool now exists
+    ctx = mp.get_context("fork")
+    q = ctx.Queue()
+    p = ctx.Process(target=_read_in_child, args=(scp, q))
+    p.start()
+    p.join(60)
+    alive = p.is_alive()
+    if alive:
+        p.kill()
+    assert not alive and p.exitcode == 0
+    assert q.get(timeout=5) == float(np.abs(b).sum())

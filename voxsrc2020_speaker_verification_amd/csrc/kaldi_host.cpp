@@ -23,6 +23,8 @@
 #include <thread>
 #include <vector>
 
+#include <unistd.h>
+
 #include "../../include/voxemb.h"
 
 int vox_set_error(int code, const char* msg);  // api.cpp (shared thread-local message)
@@ -442,6 +444,26 @@ class WorkerPool {
   bool stop_ = false;
 };
 
+// The calling thread's pool.  A forked child (Python multiprocessing's default
+// start method) inherits the object but none of its worker threads, and would
+// wait for them forever: a pool made in another process is abandoned (leaked --
+// its threads cannot be joined here) and a new one started.
+struct PoolHolder {
+  WorkerPool* p = nullptr;
+  pid_t pid = 0;
+  ~PoolHolder() {
+    if (p && pid == getpid()) delete p;
+  }
+  WorkerPool& get() {
+    const pid_t me = getpid();
+    if (!p || pid != me) {
+      p = new WorkerPool();
+      pid = me;
+    }
+    return *p;
+  }
+};
+
 template <typename F>
 int parallel_for(int n, int threads, F&& body) noexcept {
   threads = std::max(1, std::min(threads, n));
@@ -459,9 +481,9 @@ int parallel_for(int n, int threads, F&& body) noexcept {
     work();
   } else {
     try {
-      static thread_local WorkerPool pool;
+      static thread_local PoolHolder pool;
       const std::function<void()> job = work;
-      pool.run(threads, job);
+      pool.get().run(threads, job);
     } catch (...) {
       work();   // no pool (allocation failed): the calling thread alone
     }
