@@ -314,7 +314,7 @@ class LanePool:
         F, dim = self.table.feat_dim, ex.dim
         prev = None              # (bid, n, done event, pinned output)
         free = [None, None]      # event after the H2D that last read h_in[k][j]
-        used = [None, None]      # event after the D2D that last read d_stage[k][j]
+        used = [None, None]      # event after the forward that last read d_stage / d_len[k][j]
         clock, ph = time.perf_counter, {"read": 0.0, "launch": 0.0, "wait": 0.0}
         try:
             torch.cuda.set_device(self.dev)
@@ -349,14 +349,16 @@ class LanePool:
                 s.wait_event(free[j])
                 with torch.cuda.stream(s):
                     x.copy_(xs)
-                    used[j] = torch.cuda.Event()
-                    used[j].record(s)
                 if self.ragged:
                     ex.run_device_lens(x.view(n, L, F), dl, o.view(n, dim), s)
                 else:
                     ex.run_device(x.view(n, L, F), o.view(n, dim), s)
                 h = self.h_out[k][j]
                 with torch.cuda.stream(s):
+                    # after the forward, which also reads d_len[k][j] (copied into
+                    # the plan's workspace on s): the copy stream may refill both
+                    used[j] = torch.cuda.Event()
+                    used[j].record(s)
                     h[:n * dim].copy_(o, non_blocking=True)
                     done = torch.cuda.Event()
                     done.record(s)
