@@ -265,13 +265,14 @@ class SyncRunner:
 class LanePool:
     """`lanes` extraction handles on one device, each driven by its own host
     thread: lane k takes batches k, k + K, k + 2K, ...; for each it reads the
-    chunks into one of its two pinned buffers with the native reader (the
-    GIL is released in every native call, so the lanes' reading, planning and
-    launching run in parallel), queues the H2D on its copy stream (into one of
-    two device buffers) and the forward + D2H on its compute stream, and then
-    finishes its previous batch -- so every lane keeps two batches in flight,
-    the host work of one hides behind the GPU work of the other, and a batch's
-    PCIe transfer overlaps the previous batch's forward."""
+    chunks into one of its two pinned buffers with the native reader on the
+    lane's reader thread (the GIL is released in every native call, so reading,
+    planning and launching run in parallel), queues the H2D on its copy stream
+    (into one of two device buffers) and the forward + D2H on its compute
+    stream, and then finishes its previous batch -- so every lane keeps two
+    batches in flight, batch i + 1 is read while batch i is queued and batch
+    i - 1 collected, and a batch's PCIe transfer overlaps the previous batch's
+    forward."""
 
     def __init__(self, extractors, table, batches, cmn=True):
         import torch
@@ -309,33 +310,46 @@ class LanePool:
         self.phase = {"read": 0.0, "launch": 0.0, "wait": 0.0}
         self._lock = threading.Lock()
 
+    def _read(self, k, j, batch, free_ev):
+        """Batch `batch` into lane k's pinned buffers j (the lane's reader thread)
+        once the H2D that last read them (free_ev) is done."""
+        if free_ev is not None:
+            free_ev.synchronize()
+        L, items = batch[0], batch[1]
+        hin = self.h_in[k][j]
+        if self.ragged:
+            self.table.read_ragged(items, batch[2], L, hin, self.cmn, self.threads)
+            self.h_len[k][j][:len(items)].copy_(self.torch.tensor(batch[2], dtype=self.torch.int32))
+        else:
+            self.table.read(items, L, hin, self.cmn, self.threads)
+
     def _lane(self, k, batches, results, stop):
+        from concurrent.futures import ThreadPoolExecutor
         torch, ex, s, cs = self.torch, self.exs[k], self.streams[k], self.copy_streams[k]
         F, dim = self.table.feat_dim, ex.dim
+        mine = list(range(k, len(batches), len(self.exs)))
         prev = None              # (bid, n, done event, pinned output)
         free = [None, None]      # event after the H2D that last read h_in[k][j]
         used = [None, None]      # event after the forward that last read d_stage / d_len[k][j]
         clock, ph = time.perf_counter, {"read": 0.0, "launch": 0.0, "wait": 0.0}
+        # the lane's reader thread reads batch i + 1 (native, GIL released) while
+        # this thread queues batch i and collects batch i - 1
+        reader = ThreadPoolExecutor(1)
+        fut = None
         try:
             torch.cuda.set_device(self.dev)
-            for i, b in enumerate(range(k, len(batches), len(self.exs))):
+            if mine:
+                fut = reader.submit(self._read, k, 0, batches[mine[0]], None)
+            for i, b in enumerate(mine):
                 if stop:
                     return
                 L, items = batches[b][0], batches[b][1]
                 n, j = len(items), i & 1
-                t0 = clock()
-                if free[j] is not None:
-                    free[j].synchronize()
                 t1 = clock()
-                hin = self.h_in[k][j]
-                if self.ragged:
-                    lens = batches[b][2]
-                    self.table.read_ragged(items, lens, L, hin, self.cmn, self.threads)
-                    hl = self.h_len[k][j]
-                    hl[:n].copy_(torch.tensor(lens, dtype=torch.int32))
-                else:
-                    self.table.read(items, L, hin, self.cmn, self.threads)
+                fut.result()                      # batch b is in h_in[k][j]
+                fut = None
                 t2 = clock()
+                hin, hl = self.h_in[k][j], self.h_len[k][j]
                 xs, x = self.d_stage[k][j][:n * L * F], self.d_in[k][:n * L * F]
                 o, dl = self.d_out[k][:n * dim], self.d_len[k][j][:n]
                 with torch.cuda.stream(cs):
@@ -346,6 +360,8 @@ class LanePool:
                         dl.copy_(hl[:n], non_blocking=True)
                     free[j] = torch.cuda.Event()
                     free[j].record(cs)
+                if i + 1 < len(mine):
+                    fut = reader.submit(self._read, k, j ^ 1, batches[mine[i + 1]], free[j ^ 1])
                 s.wait_event(free[j])
                 with torch.cuda.stream(s):
                     x.copy_(xs)
@@ -366,7 +382,7 @@ class LanePool:
                 if prev is not None:
                     results.put(self._finish(prev, dim))
                 prev = (b, n, done, h)
-                ph["wait"] += clock() - t3 + t1 - t0
+                ph["wait"] += clock() - t3
                 ph["read"] += t2 - t1
                 ph["launch"] += t3 - t2
             if prev is not None:
@@ -374,6 +390,12 @@ class LanePool:
         except BaseException as e:   # surfaced by run() on the consuming thread
             results.put(e)
         finally:
+            if fut is not None:       # a read in flight writes this lane's buffers
+                try:
+                    fut.result()
+                except BaseException:
+                    pass
+            reader.shutdown(wait=True)
             with self._lock:
                 for key, v in ph.items():
                     self.phase[key] += v
