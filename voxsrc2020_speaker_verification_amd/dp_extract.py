@@ -204,8 +204,9 @@ def main(argv=None):
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--cohort-spk2utt", default=None)
-    ap.add_argument("--lanes", type=int, default=4,
-                    help="concurrent extraction handles / streams per GPU (each its own "
+    ap.add_argument("--lanes", type=int, default=0,
+                    help="concurrent extraction handles / streams per GPU (0: 1 for the TDNN, "
+                         "4 for the 2-D conv models; each its own "
                          "weights + a workspace for the largest batch: see extract --help)")
     ap.add_argument("--reader-threads", type=int, default=None)
     ap.add_argument("--resume", action="store_true",

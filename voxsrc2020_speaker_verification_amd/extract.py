@@ -73,9 +73,17 @@ def extract_scp(scp_path, embed_batch, dim, batch=64, cmn=True, threads=None):
 
 
 def open_lanes(pb_file, device, precision, lanes):
-    """`lanes` extraction handles of one model on one device (stream.LanePool)."""
+    """`lanes` extraction handles of one model on one device (stream.LanePool).
+    lanes <= 0: automatic -- one lane for a 1-D conv model (the TDNN: its
+    forward is so short that a second lane's launches only contend for the
+    Python interpreter with the first's, profiles/r06g_extract_ragged_tdnn.json),
+    four for the 2-D conv models (GPU-bound; extra lanes cover the host gaps)."""
     from .extractor import Extractor
-    return [Extractor(pb_file, device=device, precision=precision) for _ in range(max(1, lanes))]
+    first = Extractor(pb_file, device=device, precision=precision)
+    if lanes <= 0:
+        lanes = 1 if first.expand_dim == 2 else 4
+    return [first] + [Extractor(pb_file, device=device, precision=precision)
+                      for _ in range(lanes - 1)]
 
 
 def write_vectors(base, keys, emb, atomic=False):
@@ -97,8 +105,9 @@ def main(argv=None):
     ap.add_argument("--device", type=int, default=0)
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--no-cmn", action="store_true", help="features are already CMN'd")
-    ap.add_argument("--lanes", type=int, default=4,
-                    help="concurrent extraction handles / streams per GPU.  Each lane is a "
+    ap.add_argument("--lanes", type=int, default=0,
+                    help="concurrent extraction handles / streams per GPU (0: 1 for the TDNN, "
+                         "4 for the 2-D conv models).  Each lane is a "
                          "full handle with its own copy of the weights and a workspace sized "
                          "for the largest batch (--batch x 1000 frames: ~5.6 GB for res2net50 at "
                          "--batch 64), so device memory grows with the lane count.  The lanes' "
