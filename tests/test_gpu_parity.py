@@ -890,3 +890,31 @@ def test_stream_lanes_equal_in_memory_path(weights, tmp_path, lanes, ragged):
     assert keys == [k for k, _ in mats]
     assert np.array_equal(got, ref)
     assert sum(s["built"] for s in stats) >= 1
+
+
+def test_stream_many_batches_lanes_bitwise(weights, tmp_path):
+    """Many small ragged batches in flight on two lanes (copy streams, staging
+    buffers, reader threads one batch ahead): the arks equal a one-lane run's
+    bits, twice over (a buffer reused before its last reader finished would
+    show up as a mismatch), TDNN bf16."""
+    from voxsrc2020_speaker_verification_amd import kaldi
+    from voxsrc2020_speaker_verification_amd.stream import extract_entries
+    spec, t, blob = weights("tdnn", 80)
+    rng = np.random.default_rng(21)
+    lens = rng.integers(25, 2600, 240)
+    mats = [(f"u{i:03d}", (rng.standard_normal((int(T), 80)) * 2 + 1).astype(np.float32))
+            for i, T in enumerate(lens)]
+    scp = _write_fm_ark(str(tmp_path / "f.ark"), mats)
+    (tmp_path / "f.scp").write_text("".join(scp))
+    entries = kaldi.read_scp(str(tmp_path / "f.scp"))
+    one = [_extractor(blob, "bf16")]
+    two = [_extractor(blob, "bf16") for _ in range(2)]
+    try:
+        _, ref = extract_entries(entries, one, batch=8, ragged=True)
+        for _ in range(2):
+            keys, got = extract_entries(entries, two, batch=8, ragged=True)
+            assert keys == [k for k, _ in mats]
+            assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    finally:
+        for e in one + two:
+            e.close()
