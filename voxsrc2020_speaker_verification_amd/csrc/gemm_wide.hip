@@ -872,7 +872,13 @@ hipError_t launch_gemm_wide(const ConvParams& p0, int num_cu, int variant, hipSt
   G = G >= 8 ? G / 8 * 8 : G;   // small launches (any_m) keep their few tiles
   const size_t lds = GW_NST * GW_SLOT + 8 * (size_t)p.coutp + (p.in_mean ? 8 * (size_t)p.kp : 0);
   // (the 320-wide tile holds 80 accumulators per compute wave at 128 pixels)
-  const int bm = bn == 320 ? 128 : ws_bm(M, p.coutp / bn, bn, num_cu);
+  int bm = bn == 320 ? 128 : ws_bm(M, p.coutp / bn, bn, num_cu);
+#ifdef VOX_DIAG
+  // (diagnostic VOXEMB_GEMM_VAR 37: 128-pixel tiles, one k-step per slot, on
+  // every launch -- the same results; tests the per-CU intake model, whose
+  // operand bytes per output grow by (128 + BN) / (BM + BN) * BM / 128)
+  if (variant == 37 && bn != 320) bm = 128;
+#endif
   auto grid_for = [&](int bmx) {
     const int t = ((M + bmx - 1) / bmx) * (p.coutp / bn);
     int g = num_cu < t ? num_cu : t;
@@ -882,7 +888,7 @@ hipError_t launch_gemm_wide(const ConvParams& p0, int num_cu, int variant, hipSt
   // two k-steps per ring slot on the 128-pixel tiles (few-tile launches) when
   // the three 2 x (BN + 128) x 64 B slots fit
   const size_t lds2 = 3 * 2 * (size_t)(bn + 128) * 64 + 8 * (size_t)p.coutp;
-  const bool two = ksub_on && bm == 128 && bn <= 256 && !p.in_mean &&
+  const bool two = ksub_on && variant != 37 && bm == 128 && bn <= 256 && !p.in_mean &&
                    (p.kp / 32) % 2 == 0 && lds2 <= 163840;
   if (p.in_mean || p.kh > 1) {
     // operand variants (GS_PRO / GS_TAPS): wave-specialised only
@@ -918,7 +924,7 @@ hipError_t launch_gemm_wide(const ConvParams& p0, int num_cu, int variant, hipSt
   // VOXEMB_GEMM_VAR=-1 selects gemm1x1_wide
   if (variant == 0) variant = 1;
   if (variant == -1) variant = 0;
-  if (variant == 1 || (variant >= 21 && variant <= 36)) {   // wave-specialised
+  if (variant == 1 || (variant >= 21 && variant <= 37)) {   // wave-specialised
     auto go = [&](auto dbgc) {
       constexpr int D = decltype(dbgc)::value;
       if (two && bn == 192) {
