@@ -117,6 +117,16 @@ def test_reader_errors_are_reported(tmp_path):
     t = ChunkTable([lines[0].split()], threads=1)
     with pytest.raises(_native.VoxError):
         t.read([(0, 0, 30)], 20, np.empty(20 * 8, np.float32))   # chunk past the end
+    # ragged reads: a length outside [1, stride], a chunk past the end -- through
+    # the worker pool (threads > 1) as well as on the calling thread
+    buf = np.zeros(2 * 32 * 8, np.float32)
+    for threads in (1, 4):
+        for items, lens, stride in ([[(0, 0, 0), (0, 0, 5)], [33, 10], 32],
+                                    [[(0, 0, 0), (0, 0, 5)], [10, 0], 32],
+                                    [[(0, 0, 0), (0, 0, 35)], [10, 10], 32]):
+            with pytest.raises(_native.VoxError):
+                t.read_ragged(items, lens, stride, buf, threads=threads)
+        t.read_ragged([(0, 0, 0), (0, 0, 5)], [32, 10], 32, buf, threads=threads)   # still usable
 
 
 def test_plan_batches_ragged():
