@@ -188,6 +188,25 @@ int vox_sliding_cmn_device(const float* d_in, const int64_t* d_frame_off, int n_
 int64_t vox_cm_blob_bytes(int rows, int cols);
 int vox_cm_compress_device(const float* d_in, const int64_t* d_frame_off, int n_utt, int f,
                            uint8_t* d_blob, const int64_t* d_blob_off, float* d_out, void* stream);
+/* The device side of the extraction reader (tf_extract.py:63: apply-cmvn-sliding
+ * over the `copy-feats --compress` arks, prepare_data.sh:69), the GPU form of
+ * vox_read_chunks(_ragged) for "CM " matrices: U payloads as
+ * vox_read_cm_payloads reads them are decoded in Kaldi C++'s arithmetic
+ * (bit-identical to vox_read_mat_kaldi), sliding-window CMN'd when
+ * cmn_window > 0 (centered; bit-identical to vox_sliding_cmn), and n_items
+ * chunks gathered into d_out [n_items][stride][f] (rows past a chunk's length
+ * zero).  d_meta (device int64): blob_off[U+1] | frame_off[U+1] | rows[U] |
+ * item_utt[n] | item_start[n] | item_len[n]; utterance u's payload at
+ * d_blob + blob_off[u] holds rows[u] rows, of which the first need[u] =
+ * frame_off[u+1] - frame_off[u] are decoded (total_rows = frame_off[U],
+ * max_need = the largest need).  The CMN windows of a chunk's rows must lie in
+ * the decoded rows: need = min(rows, max(end + cmn_window - cmn_window/2,
+ * cmn_window)) for the utterance's last chunk end `end` (need = end without
+ * CMN).  d_work: 2 * total_rows * f floats (total_rows * f without CMN).
+ * Asynchronous on `stream`; U <= 65535. */
+int vox_cm_chunks_device(const uint8_t* d_blob, const int64_t* d_meta, int n_utt,
+                         int64_t total_rows, int max_need, int n_items, int stride, int f,
+                         int cmn_window, float* d_work, float* d_out, void* stream);
 
 const char* vox_last_error(void);
 
@@ -253,6 +272,15 @@ int vox_read_chunks(const char* const* paths, const int64_t* offsets, const int*
 int vox_read_chunks_ragged(const char* const* paths, const int64_t* offsets, const int* r0,
                            const int* T, const int* c0, const int* start, const int* lens, int n,
                            int f, int stride, int cmn_window, float* out, int threads);
+/* Matrix kinds at paths[i]:offsets[i] (headers only): 0 "FM", 1 "DM", 2 "CM",
+ * 3 "CM2". */
+int vox_mat_kinds(const char* const* paths, const int64_t* offsets, int n, int* kinds, int threads);
+/* The raw "CM " payloads (the bytes after the token) of n matrices into buf:
+ * payload i at buf + blob_off[i], blob_off[i+1] - blob_off[i] = 16 + 8 cols +
+ * rows cols bytes (rows > 8) -- the input of vox_cm_chunks_device.  VOX_EINVAL
+ * when a matrix is not "CM " with those dimensions. */
+int vox_read_cm_payloads(const char* const* paths, const int64_t* offsets, int n,
+                         const int64_t* blob_off, int cols, uint8_t* buf, int threads);
 /* Serialise "key \0BFV \4<u32 dim><dim f32>" into buf; returns bytes written
  * (or needed, if cap is too small) and the offset of "\0B" via *data_offset. */
 int64_t vox_format_vec_flt(const char* key, const float* v, int dim, uint8_t* buf,

@@ -73,8 +73,10 @@ def child(args):
     t_plan = time.perf_counter() - t0
     pools = []
 
+    devread = {"auto": None, "host": False, "device": True}[args.reader]
+
     def make_pool(b):
-        pools.append(stream.LanePool(lanes, table, b))
+        pools.append(stream.LanePool(lanes, table, b, device_reader=devread))
         return pools[-1]
 
     keys, emb = stream.extract_stream(table, make_pool, args.batch, ragged=ragged)
@@ -101,6 +103,7 @@ def child(args):
         "seconds": round(el, 4), "plan_s": round(t_plan, 4), "write_s": round(t_write, 4),
         "utt_per_s": round(len(keys) / el, 1), "frames_per_s": round(frames / el, 1),
         "warm_seconds": round(t_warm, 4), "warm_frames_per_s": round(frames / t_warm, 1),
+        "reader": "device" if pools[0].devread else "host",
         "lane_phase_s": {k: round(v, 4) for k, v in pools[0].phase.items()},
         "warm_lane_phase_s": {k: round(v, 4) for k, v in pools[1].phase.items()},
         "plans_built": sum(s["built"] for s in st), "plan_hits": sum(s["hits"] for s in st),
@@ -145,6 +148,8 @@ def main():
     ap.add_argument("--child", action="store_true")
     ap.add_argument("--scp", default=None)
     ap.add_argument("--wspec", default=None)
+    ap.add_argument("--reader", default="auto", choices=["auto", "host", "device"],
+                    help="decode + CMN on the host threads or on the GPU (vox_cm_chunks_device)")
     ap.add_argument("--mode", default="auto", choices=["auto", "ragged", "exact"],
                     help="ragged batches (vox_embed_lens) or equal-length batches")
     args = ap.parse_args()
@@ -167,7 +172,8 @@ def main():
                 continue   # the doubled set: RSS check at the last lane count only
             cmd = [sys.executable, os.path.abspath(__file__), "--child", "--scp", base + ".scp",
                    "--wspec", os.path.join(args.dir, f"xv{n}_{lanes}"), "--lanes", str(lanes),
-                   "--batch", str(args.batch), "--model", args.model, "--mode", args.mode]
+                   "--batch", str(args.batch), "--model", args.model, "--mode", args.mode,
+                   "--reader", args.reader]
             if args.threads:
                 cmd += ["--threads", str(args.threads)]
             r = subprocess.run(cmd, capture_output=True, text=True, cwd=ROOT)

@@ -103,6 +103,12 @@ _SIGS = [
                                          C.c_void_p, C.c_void_p, C.c_void_p]),
     ("vox_sliding_cmn_device", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int,
                                          C.c_int, C.c_void_p, C.c_void_p]),
+    ("vox_cm_chunks_device", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_int64, C.c_int,
+                                       C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
+                                       C.c_void_p]),
+    ("vox_mat_kinds", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int]),
+    ("vox_read_cm_payloads", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int,
+                                       C.c_void_p, C.c_int]),
     ("vox_format_vec_flt", C.c_int64, [C.c_char_p, _F, C.c_int, C.c_void_p, C.c_size_t,
                                        C.POINTER(C.c_int64)]),
 ]

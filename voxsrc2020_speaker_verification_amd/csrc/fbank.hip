@@ -21,6 +21,7 @@
 // utterance's frames: bit-identical to the host vox_sliding_cmn.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -228,6 +229,87 @@ __global__ void cmn_k(const float* __restrict__ in, const int64_t* __restrict__ 
     last_end = we;
     const double alpha = -1.0 / n;
     y[(long)t * F] = (float)((double)x[(long)t * F] + alpha * s);
+  }
+}
+
+// cmn_k's recursion (center = true) with its loads issued ahead: the windows
+// advance by at most one row per frame, so the rows a block of CMN_B frames
+// subtracts, adds and centres are known before any of its sums -- all 3 CMN_B
+// loads go out first, then the CMN_B dependent double updates run in cmn_k's
+// order.  One thread per (utterance, bin) still, so the frames are a serial
+// chain; cmn_k waited out a load round trip per frame.
+constexpr int CMN_B = 32;   // <= 64: the per-frame flags are 64-bit masks
+static_assert(CMN_B <= 64, "flag masks");
+__global__ __launch_bounds__(256) void cmn_fast_k(const float* __restrict__ in,
+                                                  const int64_t* __restrict__ frame_off,
+                                                  int n_utt, int F, int W,
+                                                  float* __restrict__ out) {
+  const long id = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= (long)n_utt * F) return;
+  const int u = (int)(id / F), c = (int)(id - (long)u * F);
+  const int64_t base = frame_off[u];
+  const int T = (int)(frame_off[u + 1] - base);
+  if (T <= 0) return;
+  const float* __restrict__ x = in + base * F + c;   // row r at x[r * F] (T * F < 2^31)
+  float* __restrict__ y = out + base * F + c;
+  // Kaldi's centred window of frame t, branch-free: [max(t - W/2, 0), + W),
+  // shifted left (not below 0) to end at T
+  auto win = [&](int t, int& ws, int& we) {
+    const int a = max(t - W / 2, 0);
+    const bool over = a + W > T;
+    ws = over ? max(T - W, 0) : a;
+    we = over ? T : a + W;
+  };
+  int ls, le;
+  win(0, ls, le);
+  double s = 0.0;
+  for (int r = ls; r < le; r += CMN_B) {   // the first window, in row order
+    float v[CMN_B];
+#pragma unroll
+    for (int k = 0; k < CMN_B; ++k) v[k] = x[min(r + k, T - 1) * F];
+#pragma unroll
+    for (int k = 0; k < CMN_B; ++k)
+      if (r + k < le) s += (double)v[k];
+  }
+  int n_prev = -1;
+  double alpha = 0.0;
+  for (int t = 0; t < T; t += CMN_B) {
+    // every row this block of frames subtracts, adds and centres, requested first
+    float xs[CMN_B], xa[CMN_B], xt[CMN_B];
+    uint64_t dsub = 0, dadd = 0, nchg = 0;   // one bit per frame of the block
+    int ps = ls, pe = le, pn = le - ls;
+#pragma unroll
+    for (int k = 0; k < CMN_B; ++k) {
+      const int tt = t + k;
+      int ws = ps, we = pe;
+      if (tt > 0) win(min(tt, T - 1), ws, we);
+      dsub |= (uint64_t)(ws > ps) << k;
+      dadd |= (uint64_t)(we > pe) << k;
+      xs[k] = x[ps * F];
+      xa[k] = x[min(pe, T - 1) * F];
+      xt[k] = x[min(tt, T - 1) * F];
+      nchg |= (uint64_t)(we - ws != pn) << k;
+      pn = we - ws;
+      ps = ws;
+      pe = we;
+    }
+#pragma unroll
+    for (int k = 0; k < CMN_B; ++k) {
+      if (t + k >= T) break;
+      if ((dsub >> k) & 1) s -= (double)xs[k];
+      if ((dadd >> k) & 1) s += (double)xa[k];
+      // the window size is W away from the utterance edges: its -1/n (an IEEE
+      // double division, a long dependent sequence) only when it changes
+      if (n_prev < 0 || ((nchg >> k) & 1)) {
+        int ws, we;
+        win(t + k, ws, we);
+        n_prev = we - ws;
+        alpha = -1.0 / n_prev;
+      }
+      y[(t + k) * F] = (float)((double)xt[k] + alpha * s);
+    }
+    ls = ps;
+    le = pe;
   }
 }
 
@@ -601,12 +683,85 @@ extern "C" int vox_sliding_cmn_device(const float* d_in, const int64_t* d_frame_
   if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(at.device) != hipSuccess)
     return vox_set_error(VOX_EHIP, "cmn: cannot select the features' device");
   const long threads = (long)n_utt * f;
-  hipLaunchKernelGGL(cmn_k, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, d_in, d_frame_off, n_utt, f, cmn_window, center, d_out);
+  if (center)
+    hipLaunchKernelGGL(cmn_fast_k, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, d_in, d_frame_off, n_utt, f, cmn_window, d_out);
+  else
+    hipLaunchKernelGGL(cmn_k, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, d_in, d_frame_off, n_utt, f, cmn_window, center, d_out);
   hipError_t e = hipGetLastError();
   (void)hipSetDevice(prev);
   if (e != hipSuccess) return vox_set_error(VOX_EHIP, (std::string("cmn_k: ") + hipGetErrorString(e)).c_str());
   return VOX_OK;
+}
+
+// ---- device side of the extraction reader: CM payloads -> decoded rows ->
+// sliding CMN -> the padded chunk batch (tf_extract.py:63, the values
+// apply-cmvn-sliding computes from `copy-feats --compress` arks; the host
+// reader's arithmetic, kaldi_host.cpp parse_payload with cm_kaldi = 1).
+// meta (int64): blob_off[U+1] | frame_off[U+1] | rows[U] | item_utt[n] | item_start[n] | item_len[n]
+// Utterance u: its payload at blob + blob_off[u] (rows[u] rows, column-major
+// bytes), rows [0, frame_off[u+1] - frame_off[u]) of it decoded.
+
+// rows [64 blockIdx.x, +64) of utterance blockIdx.y: the column percentiles to
+// LDS, the bytes read column-major (coalesced per column), the floats written
+// row-major through an LDS tile
+constexpr int CMD_R = 64;
+__global__ __launch_bounds__(256) void cm_rows_k(const uint8_t* __restrict__ blob,
+                                                 const int64_t* __restrict__ meta, int U, int F,
+                                                 float* __restrict__ out) {
+  const int u = blockIdx.y, tid = threadIdx.x;
+  const int64_t* blob_off = meta;
+  const int64_t* frame_off = meta + U + 1;
+  const int64_t* rows = meta + 2 * (U + 1);
+  const int64_t base = frame_off[u];
+  const int need = (int)(frame_off[u + 1] - base);
+  const int r0 = blockIdx.x * CMD_R;
+  if (r0 >= need) return;
+  const int T = (int)rows[u];
+  const uint8_t* b = blob + blob_off[u];
+  extern __shared__ float cm_lds[];
+  float* pc = cm_lds;                 // [F][4] column percentiles
+  float* tile = cm_lds + 4 * F;       // [CMD_R][F + 1]
+  float hdr[2];
+  __builtin_memcpy(hdr, b, 8);
+  for (int i = tid; i < 4 * F; i += 256) {
+    uint16_t v;
+    __builtin_memcpy(&v, b + 16 + 2 * i, 2);
+    pc[i] = cm_f16(hdr[0], hdr[1], v);
+  }
+  __syncthreads();
+  const int nr = min(CMD_R, need - r0);
+  const uint8_t* data = b + 16 + 8 * F;
+  for (int i = tid; i < F * CMD_R; i += 256) {
+    const int c = i / CMD_R, r = i - c * CMD_R;
+    if (r < nr) {
+      const int v = data[(int64_t)c * T + r0 + r];
+      tile[r * (F + 1) + c] = cm_unchar(pc[4 * c], pc[4 * c + 1], pc[4 * c + 2], pc[4 * c + 3], v);
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < F * nr; i += 256) {
+    const int r = i / F, c = i - r * F;
+    out[(base + r0 + r) * F + c] = tile[r * (F + 1) + c];
+  }
+}
+
+// item i's rows [start, start + len) of its utterance into rows [i stride, + len)
+// of the batch, zero up to the stride
+__global__ __launch_bounds__(256) void chunk_gather_k(const float* __restrict__ feats,
+                                                      const int64_t* __restrict__ meta, int U, int n,
+                                                      int stride, int F, float* __restrict__ out) {
+  const int64_t* frame_off = meta + U + 1;
+  const int64_t* it = meta + 3 * U + 2;   // item_utt | item_start | item_len
+  const int64_t total = (int64_t)n * stride * F;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int64_t row = e / F;
+    const int c = (int)(e - row * F);
+    const int i = (int)(row / stride), t = (int)(row - (int64_t)i * stride);
+    const int u = (int)it[i];
+    out[e] = t < it[2 * n + i] ? feats[(frame_off[u] + it[n + i] + t) * F + c] : 0.f;
+  }
 }
 
 extern "C" int64_t vox_cm_blob_bytes(int rows, int cols) {
@@ -635,5 +790,41 @@ extern "C" int vox_cm_compress_device(const float* d_in, const int64_t* d_frame_
   (void)hipSetDevice(prev);
   if (e != hipSuccess)
     return vox_set_error(VOX_EHIP, (std::string("cm kernels: ") + hipGetErrorString(e)).c_str());
+  return VOX_OK;
+}
+
+extern "C" int vox_cm_chunks_device(const uint8_t* d_blob, const int64_t* d_meta, int n_utt,
+                                    int64_t total_rows, int max_need, int n_items, int stride,
+                                    int f, int cmn_window, float* d_work, float* d_out,
+                                    void* stream) {
+  if (!d_blob || !d_meta || !d_work || !d_out || n_utt <= 0 || n_utt > 65535 || total_rows <= 0 ||
+      max_need <= 0 || n_items <= 0 || stride <= 0 || f <= 0 || f > 2048 || cmn_window < 0)
+    return vox_set_error(VOX_EINVAL, "bad cm chunk arguments");
+  hipPointerAttribute_t at;
+  if (hipPointerGetAttributes(&at, d_out) != hipSuccess || at.type != hipMemoryTypeDevice)
+    return vox_set_error(VOX_EINVAL, "cm chunks: the batch must be device memory");
+  int prev = -1;
+  if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(at.device) != hipSuccess)
+    return vox_set_error(VOX_EHIP, "cm chunks: cannot select the batch's device");
+  hipStream_t s = (hipStream_t)stream;
+  const size_t lds = (size_t)(4 * f + CMD_R * (f + 1)) * 4;
+  hipLaunchKernelGGL(cm_rows_k, dim3((unsigned)((max_need + CMD_R - 1) / CMD_R), (unsigned)n_utt),
+                     dim3(256), lds, s, d_blob, d_meta, n_utt, f, d_work);
+  const float* feats = d_work;
+  if (cmn_window > 0) {
+    float* cm = d_work + (size_t)total_rows * f;   // the CMN'd rows follow the decoded ones
+    const long threads = (long)n_utt * f;
+    hipLaunchKernelGGL(cmn_fast_k, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, d_work,
+                       d_meta + n_utt + 1, n_utt, f, cmn_window, cm);
+    feats = cm;
+  }
+  const int64_t total = (int64_t)n_items * stride * f;
+  const unsigned g = (unsigned)std::min<int64_t>((total + 255) / 256, 8192);
+  hipLaunchKernelGGL(chunk_gather_k, dim3(g), dim3(256), 0, s, feats, d_meta, n_utt, n_items,
+                     stride, f, d_out);
+  hipError_t e = hipGetLastError();
+  (void)hipSetDevice(prev);
+  if (e != hipSuccess)
+    return vox_set_error(VOX_EHIP, (std::string("cm chunk kernels: ") + hipGetErrorString(e)).c_str());
   return VOX_OK;
 }

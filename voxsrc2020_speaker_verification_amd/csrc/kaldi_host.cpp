@@ -499,7 +499,7 @@ int parallel_for(int n, int threads, F&& body) noexcept {
 }
 
 // header only (no payload read): rows / cols of the matrix at path:offset
-int read_shape_at(const char* path, int64_t offset, int* rows, int* cols) {
+int read_shape_at(const char* path, int64_t offset, int* rows, int* cols, int* kind = nullptr) {
   FILE* f = std::fopen(path, "rb");
   if (!f) return kfail(VOX_EIO, "cannot open matrix file");
   uint8_t head[64];
@@ -508,10 +508,65 @@ int read_shape_at(const char* path, int64_t offset, int* rows, int* cols) {
   std::fclose(f);
   if (got == 0) return kfail(VOX_EIO, "offset beyond end of file");
   Reader r{head, got};
-  int kind;
-  return parse_header(r, rows, cols, &kind);
+  int k;
+  const int rc = parse_header(r, rows, cols, &k);
+  if (kind) *kind = k;
+  return rc;
 }
 }  // namespace
+
+extern "C" int vox_mat_kinds(const char* const* paths, const int64_t* offsets, int n, int* kinds,
+                             int threads) {
+  if (n < 0 || (n > 0 && (!paths || !offsets || !kinds))) return kfail(VOX_EINVAL, "null argument");
+  FirstError err;
+  const int prc = parallel_for(n, threads, [&](int i) {
+    if (err.code.load()) return;
+    int r, c;
+    const int rc = paths[i] ? read_shape_at(paths[i], offsets[i], &r, &c, &kinds[i])
+                            : kfail(VOX_EINVAL, "null path");
+    if (rc) err.set(rc, (std::string(paths[i] ? paths[i] : "?") + ": " + vox_last_error()).c_str());
+  });
+  if (err.code.load()) return kfail(err.code.load(), err.msg.c_str());
+  return prc;
+}
+
+// The CM payloads (what follows each "\0B" "CM " header token) of n matrices
+// into buf: payload i at buf + blob_off[i], blob_off[i+1] - blob_off[i] =
+// 16 + 8 cols + rows cols bytes.  Nothing is decoded: the device does that
+// (vox_cm_chunks_device).  A matrix that is not "CM " with those dimensions
+// (rows > 8) is VOX_EINVAL, so the caller can fall back to the host reader.
+extern "C" int vox_read_cm_payloads(const char* const* paths, const int64_t* offsets, int n,
+                                    const int64_t* blob_off, int cols, uint8_t* buf, int threads) {
+  if (n < 0 || cols <= 0 || (n > 0 && (!paths || !offsets || !blob_off || !buf)))
+    return kfail(VOX_EINVAL, "null argument");
+  FirstError err;
+  const int prc = parallel_for(n, threads, [&](int i) {
+    if (err.code.load()) return;
+    auto bad = [&](int rc) {
+      err.set(rc, (std::string(paths[i] ? paths[i] : "?") + ": " + vox_last_error()).c_str());
+    };
+    const int64_t size = blob_off[i + 1] - blob_off[i];
+    const int64_t rows = (size - 16 - 8 * (int64_t)cols) / cols;
+    if (!paths[i] || size <= 16 + 8 * (int64_t)cols || rows <= 8 || rows > (1 << 30) ||
+        16 + 8 * (int64_t)cols + rows * cols != size)
+      return bad(kfail(VOX_EINVAL, "bad CM payload size"));
+    FILE* f = std::fopen(paths[i], "rb");
+    if (!f) return bad(kfail(VOX_EIO, "cannot open matrix file"));
+    uint8_t tok[5];
+    uint8_t* dst = buf + blob_off[i];
+    const bool ok = offsets[i] >= 0 && std::fseek(f, (long)offsets[i], SEEK_SET) == 0 &&
+                    std::fread(tok, 1, 5, f) == 5 && std::fread(dst, 1, (size_t)size, f) == (size_t)size;
+    std::fclose(f);
+    if (!ok) return bad(kfail(VOX_EIO, "short read"));
+    if (std::memcmp(tok, "\0BCM ", 5) != 0) return bad(kfail(VOX_EINVAL, "not a CM matrix"));
+    int32_t hr, hc;
+    std::memcpy(&hr, dst + 8, 4);
+    std::memcpy(&hc, dst + 12, 4);
+    if (hr != rows || hc != cols) return bad(kfail(VOX_EINVAL, "CM header dimensions differ"));
+  });
+  if (err.code.load()) return kfail(err.code.load(), err.msg.c_str());
+  return prc;
+}
 
 extern "C" int vox_mat_shapes(const char* const* paths, const int64_t* offsets, int n, int* rows,
                               int* cols, int threads) {

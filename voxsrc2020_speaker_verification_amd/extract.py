@@ -114,6 +114,9 @@ def main(argv=None):
                          "streams and pinned buffers come from PyTorch (ROCm build)")
     ap.add_argument("--reader-threads", type=int, default=None,
                     help="host threads decoding + CMN'ing features (default: usable CPUs, <= 16)")
+    ap.add_argument("--device-reader", action="store_true",
+                    help="decode the CM arks and apply the sliding CMN on the GPU (whole \"CM \" "
+                         "matrices only; same bits as the host reader, about one host thread)")
     a = ap.parse_args(argv)
     import torch
     from .kaldi import read_scp
@@ -125,7 +128,8 @@ def main(argv=None):
             print(f"warning: --expand-dim {a.expand_dim} but the model layout is "
                   f"{lanes[0].expand_dim}; using the model's", file=sys.stderr)
         keys, emb = extract_entries(read_scp(a.rspec + ".scp"), lanes, a.batch,
-                                    cmn=not a.no_cmn, threads=a.reader_threads)
+                                    cmn=not a.no_cmn, threads=a.reader_threads,
+                                    device_reader=a.device_reader or None)
     finally:
         for ex in lanes:
             ex.close()

@@ -98,6 +98,8 @@ class ChunkTable:
         if n and (self.F != self.F[0]).any():
             raise ValueError("utterances with different feature dimensions in one scp")
         self.feat_dim = int(self.F[0]) if n else 0
+        self._rows, self._cols = rows, cols
+        self._cm_ok = None
 
     def __len__(self):
         return len(self.keys)
@@ -118,6 +120,63 @@ class ChunkTable:
                                     c0.ctypes.data, st.ctypes.data, n, self.feat_dim, int(L),
                                     CMN_WINDOW if cmn else 0, C.c_void_p(ptr),
                                     threads or self.threads))
+
+    def cm_device_ok(self):
+        """Every matrix a whole "CM " one (no [range]): the device reader
+        (vox_cm_chunks_device) can decode it."""
+        if self._cm_ok is None:
+            n = len(self)
+            kinds = np.zeros(n, np.int32)
+            if n:
+                check(lib().vox_mat_kinds(self._path_arr, self.offsets.ctypes.data, n,
+                                          kinds.ctypes.data, self.threads))
+            self._cm_ok = bool(n) and bool(
+                (kinds == 2).all() and (self.r0 == 0).all() and (self.c0 == 0).all() and
+                (self.T == self._rows).all() and (self.F == self._cols).all() and (self.T > 8).all())
+        return self._cm_ok
+
+    def cm_batch(self, items, lens, cmn=True):
+        """The device reader's plan of one batch: its utterances (first
+        appearance order), their payload offsets and the rows each must decode
+        (the CMN windows of the batch's chunks inside them) -> (utts, meta
+        int64 [blob_off | frame_off | rows | item_utt | item_start | item_len],
+        payload bytes, total rows, max rows)."""
+        F = self.feat_dim
+        slot, utts, hi = {}, [], []
+        iu = np.empty(len(items), np.int64)
+        for i, (u, _, st) in enumerate(items):
+            k = slot.get(u)
+            if k is None:
+                k = slot[u] = len(utts)
+                utts.append(u)
+                hi.append(0)
+            iu[i] = k
+            hi[k] = max(hi[k], st + lens[i])
+        U = len(utts)
+        T = self.T[utts].astype(np.int64)
+        hi = np.asarray(hi, np.int64)
+        need = np.minimum(T, np.maximum(hi + CMN_WINDOW - CMN_WINDOW // 2, CMN_WINDOW)) if cmn else hi
+        meta = np.empty(3 * U + 2 + 3 * len(items), np.int64)
+        meta[0] = 0
+        np.cumsum(16 + 8 * F + T * F, out=meta[1:U + 1])
+        meta[U + 1] = 0
+        np.cumsum(need, out=meta[U + 2:2 * U + 2])
+        meta[2 * U + 2:3 * U + 2] = T
+        n = len(items)
+        meta[3 * U + 2:3 * U + 2 + n] = iu
+        meta[3 * U + 2 + n:3 * U + 2 + 2 * n] = [it[2] for it in items]
+        meta[3 * U + 2 + 2 * n:] = lens
+        return utts, meta, int(meta[U]), int(meta[2 * U + 1]), int(need.max())
+
+    def read_cm_payloads(self, utts, meta, buf, threads=None):
+        """The "CM " payloads of `utts` into buf (pinned host memory) at the
+        offsets cm_batch planned."""
+        U = len(utts)
+        paths = (C.c_char_p * U)(*[self._paths[u] for u in utts])
+        offs = np.ascontiguousarray(self.offsets[utts])
+        ptr = buf.data_ptr() if hasattr(buf, "data_ptr") else buf.ctypes.data
+        check(lib().vox_read_cm_payloads(paths, offs.ctypes.data, U, meta.ctypes.data,
+                                         self.feat_dim, C.c_void_p(ptr), threads or self.threads))
 
     def read_ragged(self, items, lens, stride, out, cmn=True, threads=None):
         """Chunks [(u, ci, start)] of lens[i] frames each into rows
@@ -274,7 +333,7 @@ class LanePool:
     i - 1 collected, and a batch's PCIe transfer overlaps the previous batch's
     forward."""
 
-    def __init__(self, extractors, table, batches, cmn=True):
+    def __init__(self, extractors, table, batches, cmn=True, device_reader=None):
         import torch
         self.torch = torch
         self.exs = list(extractors)
@@ -285,6 +344,33 @@ class LanePool:
         max_n = max((len(b[1]) for b in batches), default=1)
         # ragged batches (L, items, lens): per-lane device lengths + pinned copies
         self.ragged = bool(batches) and len(batches[0]) == 3
+        # device reader (whole "CM " matrices, opt-in): the payload bytes cross
+        # PCIe and the GPU decodes, CMNs and gathers the chunks
+        # (vox_cm_chunks_device) -- a quarter of the float32 bytes and about one
+        # host thread instead of the reader's pool, at about the host reader's
+        # extraction rate (its CMN is a serial chain per (utterance, bin):
+        # DESIGN.md "Device reader")
+        if device_reader is None:
+            device_reader = False
+        if device_reader and not (bool(batches) and table.cm_device_ok()):
+            raise ValueError("the device reader needs whole \"CM \" matrices (no [range])")
+        self.devread = bool(device_reader)
+        if self.devread:
+            mb = mm = mr = 1
+            for b in batches:
+                _, meta, nbytes, total, _ = table.cm_batch(b[1], self._lens(b), cmn)
+                mb, mm, mr = max(mb, nbytes), max(mm, len(meta)), max(mr, total)
+            self.h_blob = [[torch.empty(mb, dtype=torch.uint8).pin_memory() for _ in range(2)]
+                           for _ in range(K)]
+            self.h_meta = [[torch.empty(mm, dtype=torch.int64).pin_memory() for _ in range(2)]
+                           for _ in range(K)]
+            self.d_blob = [[torch.empty(mb, dtype=torch.uint8, device=self.dev) for _ in range(2)]
+                           for _ in range(K)]
+            self.d_meta = [[torch.empty(mm, dtype=torch.int64, device=self.dev) for _ in range(2)]
+                           for _ in range(K)]
+            self.d_work = [torch.empty(2 * mr * F, dtype=torch.float32, device=self.dev)
+                           for _ in range(K)]
+            self.slot_info = [[None, None] for _ in range(K)]
         self.d_len = [[torch.empty(max_n, dtype=torch.int32, device=self.dev) for _ in range(2)]
                       for _ in range(K)]
         self.h_len = [[torch.empty(max_n, dtype=torch.int32).pin_memory() for _ in range(2)]
@@ -298,11 +384,12 @@ class LanePool:
         # into the lane's one input buffer (a D2D copy, microseconds), so the
         # resident plans, keyed on the input address, stay one per shape
         self.copy_streams = [torch.cuda.Stream(self.dev) for _ in range(K)]
+        stage = 0 if self.devread else max_el    # host float32 staging (host reader only)
         self.d_stage = [[torch.empty(max_el, dtype=torch.float32, device=self.dev)
                          for _ in range(2)] for _ in range(K)]
         self.d_in = [torch.empty(max_el, dtype=torch.float32, device=self.dev) for _ in range(K)]
         self.d_out = [torch.empty(max_n * dim, dtype=torch.float32, device=self.dev) for _ in range(K)]
-        self.h_in = [[torch.empty(max_el, dtype=torch.float32).pin_memory() for _ in range(2)]
+        self.h_in = [[torch.empty(stage, dtype=torch.float32).pin_memory() for _ in range(2)]
                      for _ in range(K)]
         self.h_out = [[torch.empty(max_n * dim, dtype=torch.float32).pin_memory() for _ in range(2)]
                       for _ in range(K)]
@@ -310,16 +397,27 @@ class LanePool:
         self.phase = {"read": 0.0, "launch": 0.0, "wait": 0.0}
         self._lock = threading.Lock()
 
+    @staticmethod
+    def _lens(batch):
+        return batch[2] if len(batch) == 3 else [batch[0]] * len(batch[1])
+
     def _read(self, k, j, batch, free_ev):
         """Batch `batch` into lane k's pinned buffers j (the lane's reader thread)
         once the H2D that last read them (free_ev) is done."""
         if free_ev is not None:
             free_ev.synchronize()
         L, items = batch[0], batch[1]
+        if self.ragged:
+            self.h_len[k][j][:len(items)].copy_(self.torch.tensor(batch[2], dtype=self.torch.int32))
+        if self.devread:
+            utts, meta, nbytes, total, mx = self.table.cm_batch(items, self._lens(batch), self.cmn)
+            self.h_meta[k][j][:len(meta)].copy_(self.torch.from_numpy(meta))
+            self.table.read_cm_payloads(utts, meta, self.h_blob[k][j], self.threads)
+            self.slot_info[k][j] = (len(utts), len(meta), nbytes, total, mx)
+            return
         hin = self.h_in[k][j]
         if self.ragged:
             self.table.read_ragged(items, batch[2], L, hin, self.cmn, self.threads)
-            self.h_len[k][j][:len(items)].copy_(self.torch.tensor(batch[2], dtype=self.torch.int32))
         else:
             self.table.read(items, L, hin, self.cmn, self.threads)
 
@@ -355,7 +453,20 @@ class LanePool:
                 with torch.cuda.stream(cs):
                     if used[j] is not None:
                         cs.wait_event(used[j])
-                    xs.copy_(hin[:n * L * F], non_blocking=True)
+                    if self.devread:
+                        # payload bytes over PCIe, then decode + CMN + gather into
+                        # the staging buffer -- on the copy stream, beside the
+                        # previous batch's forward
+                        U, nm, nbytes, total, mx = self.slot_info[k][j]
+                        self.d_blob[k][j][:nbytes].copy_(self.h_blob[k][j][:nbytes], non_blocking=True)
+                        self.d_meta[k][j][:nm].copy_(self.h_meta[k][j][:nm], non_blocking=True)
+                        check(lib().vox_cm_chunks_device(
+                            C.c_void_p(self.d_blob[k][j].data_ptr()),
+                            C.c_void_p(self.d_meta[k][j].data_ptr()), U, total, mx, n, L, F,
+                            CMN_WINDOW if self.cmn else 0, C.c_void_p(self.d_work[k].data_ptr()),
+                            C.c_void_p(xs.data_ptr()), C.c_void_p(cs.cuda_stream)))
+                    else:
+                        xs.copy_(hin[:n * L * F], non_blocking=True)
                     if self.ragged:
                         dl.copy_(hl[:n], non_blocking=True)
                     free[j] = torch.cuda.Event()
@@ -456,12 +567,15 @@ def extract_stream(table, make_runner, batch=64, ragged=False):
     return list(table.keys), comb.out
 
 
-def extract_entries(entries, extractors, batch=64, cmn=True, threads=None, ragged=None):
+def extract_entries(entries, extractors, batch=64, cmn=True, threads=None, ragged=None,
+                    device_reader=None):
     """The GPU pipeline over scp entries [(key, rxfile)] with `extractors`
     (one lane each: same device and weights) -> (keys, [N, dim] float32).
     ragged: batch chunks of different lengths together (vox_embed_lens);
     None = wherever the model's plan supports it (Extractor.supports_lengths),
-    else equal-length batches.  The embeddings are the same bits either way."""
+    else equal-length batches.  device_reader: decode + CMN on the GPU
+    (vox_cm_chunks_device; whole "CM " matrices only); None = the host reader.
+    The embeddings are the same bits either way."""
     table = ChunkTable(entries, threads)
     dim = extractors[0].dim
     if not len(table):
@@ -470,5 +584,5 @@ def extract_entries(entries, extractors, batch=64, cmn=True, threads=None, ragge
         raise ValueError(f"feature dim {table.feat_dim} != model {extractors[0].feat_dim}")
     if ragged is None:
         ragged = extractors[0].supports_lengths()
-    return extract_stream(table, lambda batches: LanePool(extractors, table, batches, cmn), batch,
-                          ragged=ragged)
+    return extract_stream(table, lambda batches: LanePool(extractors, table, batches, cmn,
+                                                          device_reader), batch, ragged=ragged)
