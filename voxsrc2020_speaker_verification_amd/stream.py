@@ -350,8 +350,6 @@ class LanePool:
         # host thread instead of the reader's pool, at about the host reader's
         # extraction rate (its CMN is a serial chain per (utterance, bin):
         # DESIGN.md "Device reader")
-        if device_reader is None:
-            device_reader = False
         if device_reader and not (bool(batches) and table.cm_device_ok()):
             raise ValueError("the device reader needs whole \"CM \" matrices (no [range])")
         self.devread = bool(device_reader)
@@ -380,8 +378,9 @@ class LanePool:
         # H2D copies on a stream of their own per lane, into two staging buffers,
         # so batch i+1's features cross PCIe while batch i computes (a fast
         # model -- the TDNN at ~1e8 frames/s -- reads ~30 GB/s of float32
-        # features); the compute stream moves a batch from its staging buffer
-        # into the lane's one input buffer (a D2D copy, microseconds), so the
+        # features; the device reader's decode / CMN / gather kernels run there
+        # too); the compute stream moves a batch from its staging buffer into
+        # the lane's one input buffer (a D2D copy, microseconds), so the
         # resident plans, keyed on the input address, stay one per shape
         self.copy_streams = [torch.cuda.Stream(self.dev) for _ in range(K)]
         stage = 0 if self.devread else max_el    # host float32 staging (host reader only)
