@@ -115,7 +115,7 @@ int vox_plan_describe(vox_model* m, const float* d_x, int n, int t, int f, char*
  * calls served by a resident plan (the current one or a cached one) without
  * re-planning, plans destroyed
  * (evicted, or dropped when the workspace grew), and plans resident now
- * (current + cached; VOXEMB_PLAN_CACHE caps the cached ones, default 16).
+ * (current + cached; VOXEMB_PLAN_CACHE caps the cached ones, default 64).
  * Any pointer may be NULL. */
 int vox_plan_stats(const vox_model* m, int64_t* built, int64_t* hits, int64_t* dropped,
                    int* resident);

@@ -259,9 +259,10 @@ struct vox_model {
   // last batches): switching to one swaps it in without re-planning or
   // re-capturing.  Every plan points into the shared grow-only slots, so a slot
   // reallocation drops them all.  VOXEMB_PLAN_CACHE = resident plans besides
-  // the current one (default 16, 0 = the single-plan behaviour)
+  // the current one (default 64: every shape of a ragged job -- ~40 padded
+  // lengths -- stays resident across passes; 0 = the single-plan behaviour)
   std::vector<PlanEntry> cache;
-  int cache_max = 16;
+  int cache_max = 64;
   // calls of the current plan so far; its graph is captured on call
   // graph_after + 1 (a shape met once -- one chunk-length bucket of real
   // extraction -- launches eagerly instead of paying capture + instantiate).

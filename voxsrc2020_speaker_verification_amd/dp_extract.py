@@ -202,13 +202,17 @@ def main(argv=None):
     ap.add_argument("--pre-split", action="store_true")
     ap.add_argument("--wspec", required=True)
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
-    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--batch", type=int, default=0,
+                    help="chunks per batch (0: 256 for the TDNN, whose launches are short, "
+                         "64 for the 2-D conv models)")
     ap.add_argument("--cohort-spk2utt", default=None)
     ap.add_argument("--lanes", type=int, default=0,
                     help="concurrent extraction handles / streams per GPU (0: 1 for the TDNN, "
                          "4 for the 2-D conv models; each its own "
                          "weights + a workspace for the largest batch: see extract --help)")
     ap.add_argument("--reader-threads", type=int, default=None)
+    ap.add_argument("--device-reader", action="store_true",
+                    help="decode + CMN on the GPU (see extract --help)")
     ap.add_argument("--resume", action="store_true",
                     help="reuse per-rank xvector.<i>.ark/.scp that already hold the rank's shard")
     ap.add_argument("--all-gather", action="store_true",
@@ -225,7 +229,7 @@ def main(argv=None):
     torch.cuda.set_device(local)
     dist.init_process_group("nccl", rank=rank, world_size=world,
                             device_id=torch.device("cuda", local))
-    from .extract import open_lanes
+    from .extract import default_batch, open_lanes
     from .kaldi import read_scp
     from .partition import shard
     from .stream import extract_entries
@@ -239,14 +243,16 @@ def main(argv=None):
         return [k for k, _ in entries(r, w)]
 
     lanes = open_lanes(a.pb_file, local, a.precision, a.lanes)
+    batch = default_batch(lanes[0], a.batch)
     try:
         # the rank's shard streamed through its lanes (stream.py): planned from
         # the matrix headers, decoded one batch of chunks at a time
-        run(rank, world, None, None, lanes[0].dim, a.wspec, batch=a.batch,
+        run(rank, world, None, None, lanes[0].dim, a.wspec, batch=batch,
             device=torch.device("cuda", local), cohort_spk2utt=a.cohort_spk2utt,
             resume=a.resume, shard_keys=keys, tag=run_tag(a.pb_file, a.precision),
-            extract_shard=lambda r, w: extract_entries(entries(r, w), lanes, a.batch,
-                                                       threads=a.reader_threads),
+            extract_shard=lambda r, w: extract_entries(entries(r, w), lanes, batch,
+                                                       threads=a.reader_threads,
+                                                       device_reader=a.device_reader or None),
             all_gather=a.all_gather)
     finally:
         for ex in lanes:

@@ -72,6 +72,12 @@ def extract_scp(scp_path, embed_batch, dim, batch=64, cmn=True, threads=None):
     return keys, (emb if emb is not None else np.zeros((0, dim), np.float32))
 
 
+def default_batch(extractor, batch):
+    """batch <= 0: 256 chunks for a 1-D conv model (the TDNN: per-batch host
+    work would otherwise rival its forward), 64 for the 2-D conv models."""
+    return batch if batch > 0 else (256 if extractor.expand_dim == 2 else 64)
+
+
 def open_lanes(pb_file, device, precision, lanes):
     """`lanes` extraction handles of one model on one device (stream.LanePool).
     lanes <= 0: automatic -- one lane for a 1-D conv model (the TDNN: its
@@ -103,7 +109,9 @@ def main(argv=None):
     ap.add_argument("--wspec", default="/tmp/xvector", help="output ark/scp base")
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--device", type=int, default=0)
-    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--batch", type=int, default=0,
+                    help="chunks per batch (0: 256 for the TDNN, whose launches are short, "
+                         "64 for the 2-D conv models)")
     ap.add_argument("--no-cmn", action="store_true", help="features are already CMN'd")
     ap.add_argument("--lanes", type=int, default=0,
                     help="concurrent extraction handles / streams per GPU (0: 1 for the TDNN, "
@@ -127,7 +135,8 @@ def main(argv=None):
         if lanes[0].expand_dim != a.expand_dim:
             print(f"warning: --expand-dim {a.expand_dim} but the model layout is "
                   f"{lanes[0].expand_dim}; using the model's", file=sys.stderr)
-        keys, emb = extract_entries(read_scp(a.rspec + ".scp"), lanes, a.batch,
+        keys, emb = extract_entries(read_scp(a.rspec + ".scp"), lanes,
+                                    default_batch(lanes[0], a.batch),
                                     cmn=not a.no_cmn, threads=a.reader_threads,
                                     device_reader=a.device_reader or None)
     finally:
