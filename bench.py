@@ -375,6 +375,12 @@ def eer_delta(device, S=64, U=16, T=200, F=80):
             "mindcf_bf16": round(res["bf16"][1], 5), "mindcf_fp32_ref": round(res["fp32"][1], 5)}
 
 
+def _progress(msg):
+    """A progress line on stderr (stdout carries the one JSON line)."""
+    if os.environ.get("RANK", "0") == "0":
+        print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1,
@@ -430,6 +436,7 @@ def main():
 
     from voxsrc2020_speaker_verification_amd.extractor import Extractor
 
+    _progress(f"{args.model} {args.precision}: weights and plan")
     blob = weights_blob(args.model, args.feat_dim, args.cache_dir)
     ex = Extractor(blob, device=dev.index, precision=args.precision)
     B, T, F = args.batch, args.frames, args.feat_dim
@@ -467,6 +474,7 @@ def main():
         el = float(tt.item())
     ms_per_step = el * 1000.0 / args.steps
     value = world * B * args.steps / el
+    _progress(f"timed {args.steps} steps: {ms_per_step:.3f} ms per step")
 
     # ---- per-kernel timing (HIP events around every launch, same stream)
     prof = ex.profile(x, reps=5, stream=stream)
@@ -544,6 +552,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        _progress("CPU baseline (bounded sample) and the fp32 like-for-like line")
         cpu = cpu_baseline(args.model, F, T, blob)
         # like for like: the CPU baseline computes in fp32, the headline in bf16;
         # the same workload through the GPU's fp32 path, a few timed steps
@@ -570,6 +579,7 @@ def main():
     # --no-cpu-baseline and so keep their dispatch lists to the timed workload)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.no_eer \
             and args.model == "res2net50_w24_s4_c32" and args.precision == "bf16":
+        _progress("synthetic-speaker EER delta")
         eer = eer_delta(dev.index, F=F)
 
     if rank == 0:

@@ -7,6 +7,8 @@ export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT"
 O=${O:-gpurun_out/round}
 mkdir -p $O
+# (the first import on a fresh box pages the image in: print as it lands)
+timeout -k 10 300 python3 -c "import torch; print('torch', torch.__version__, flush=True)" || exit $?
 timeout -k 10 400 python3 bench.py > $O/bench.json 2> $O/bench.err || exit $?
 timeout -k 10 300 python3 bench.py --precision fp32 --steps 5 --warmup 2 --no-cpu-baseline > $O/bench_fp32.json 2> $O/bench_fp32.err || exit $?
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/stats -o run -f csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline > $O/stats.log 2>&1 || exit $?
